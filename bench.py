@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): ResNet-50 bf16 synchronous all-reduce data parallelism,
+images/sec for the whole job, one process per MI355X (RCCL over xGMI).
+
+    python bench.py --gpus N --steps K --warmup W            (N=1 runs in-process)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+Weak scaling: every GPU trains a fixed per-GPU batch (default 256 images of 224x224, synthetic
+data, random-init weights).  A timed step is the full training step: forward, fused softmax-xent,
+backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD apply.  W untimed
+warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
+is the MAX over ranks; rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "images/sec (whole node) ResNet-50 sync DP at 1/2/4/8 MI355X; scaling efficiency"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--model", default="resnet50")
+    return ap.parse_known_args(argv)[0]
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    import dtg  # noqa: F401
+    from dtg.models import resnet
+    from dtg.parallel import FlatParams, DataParallel, comm
+    from dtg.optim import FusedSGD
+    from dtg import ops
+
+    rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
+    if world != a.gpus and rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.manual_seed(1234)
+    if device.type == "cuda":
+        ops.lib()  # fail loudly if the HIP kernels are missing
+    dtype = torch.bfloat16
+    model = resnet.resnet50().to(device)
+    model = model.to(memory_format=torch.channels_last)
+    flat = FlatParams(model, compute_dtype=dtype)
+    dp = DataParallel(flat, bucket_mb=a.bucket_mb)
+    dp.broadcast_parameters(0)
+    opt = FusedSGD(flat, lr=a.lr * world, momentum=0.9, weight_decay=5e-5)
+    x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
+    model.train()
+
+    def step():
+        out = model(x)
+        loss = ops.softmax_cross_entropy(out, y)
+        loss.backward()
+        dp.finish()
+        opt.step(grad_scale=dp.grad_scale)
+        return loss
+
+    for _ in range(a.warmup):
+        loss = step()
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    sync()
+    comm.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = comm.all_reduce_max(dt, device)
+    final_loss = float(loss.float().item())
+    gb = a.batch * world
+    ips = gb * a.steps / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "ResNet-50", "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": None,
+                       "image_size": a.image, "parallelism": f"dp{world}", "optimizer": "momentum-sgd (fused)",
+                       "allreduce": f"rccl bf16, {a.bucket_mb:g} MB buckets, overlapped"},
+            "final_loss": final_loss}), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

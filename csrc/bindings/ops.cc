@@ -1,0 +1,296 @@
+// PyTorch bindings for dtg's HIP kernels (module dtg._C).
+// Each wrapper validates shapes/dtypes/devices on the host (a kernel never sees an operand whose
+// shape disagrees with its grid), allocates outputs with the caching allocator and launches on the
+// current HIP stream, so everything composes with torch streams and hipGraph capture.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "dtg/kernels.h"
+
+namespace {
+
+using at::Tensor;
+using dtg::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
+#define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
+#define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " must be " #dt)
+#define CHECK_IN(x) \
+  CHECK_CUDA(x);    \
+  CHECK_CONTIG(x)
+
+bf16_t* bfp(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+const bf16_t* cbfp(const Tensor& t) { return reinterpret_cast<const bf16_t*>(t.data_ptr()); }
+template <class T>
+T* opt_ptr(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void check_flat(const Tensor& w, const Tensor& g, const c10::optional<Tensor>& mirror) {
+  CHECK_IN(w);
+  CHECK_IN(g);
+  CHECK_DT(w, at::kFloat);
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "grad must be fp32 or bf16");
+  TORCH_CHECK(g.numel() == w.numel(), "grad/param size mismatch");
+  if (mirror.has_value() && mirror->defined()) {
+    CHECK_IN(*mirror);
+    CHECK_DT(*mirror, at::kBFloat16);
+    TORCH_CHECK(mirror->numel() == w.numel(), "mirror size mismatch");
+  }
+}
+
+void check_state(const Tensor& s, const Tensor& w) {
+  CHECK_IN(s);
+  CHECK_DT(s, at::kFloat);
+  TORCH_CHECK(s.numel() == w.numel(), "optimizer state size mismatch");
+}
+
+void check_hyper(const Tensor& h) {
+  CHECK_IN(h);
+  CHECK_DT(h, at::kFloat);
+  TORCH_CHECK(h.numel() >= 2, "hyper must hold {lr, step}");
+}
+
+// ---- optimizers ----------------------------------------------------------------------------
+void sgd_apply(Tensor w, c10::optional<Tensor> mirror, Tensor g, Tensor hyper, double wd, double gscale,
+               bool zero_grad) {
+  check_flat(w, g, mirror);
+  check_hyper(hyper);
+  c10::DeviceGuard dg(w.device());
+  dtg::sgd_apply(w.data_ptr<float>(), opt_ptr<bf16_t>(mirror), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                 w.numel(), hyper.data_ptr<float>(), (float)wd, (float)gscale, zero_grad, cur_stream());
+}
+
+void momentum_apply(Tensor w, c10::optional<Tensor> mirror, Tensor g, Tensor mom, Tensor hyper, double mu, double wd,
+                    bool nesterov, double gscale, bool zero_grad) {
+  check_flat(w, g, mirror);
+  check_state(mom, w);
+  check_hyper(hyper);
+  c10::DeviceGuard dg(w.device());
+  dtg::momentum_apply(w.data_ptr<float>(), opt_ptr<bf16_t>(mirror), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                      mom.data_ptr<float>(), w.numel(), hyper.data_ptr<float>(), (float)mu, (float)wd, nesterov,
+                      (float)gscale, zero_grad, cur_stream());
+}
+
+void adagrad_apply(Tensor w, c10::optional<Tensor> mirror, Tensor g, Tensor acc, Tensor hyper, double eps,
+                   double gscale, bool zero_grad) {
+  check_flat(w, g, mirror);
+  check_state(acc, w);
+  check_hyper(hyper);
+  c10::DeviceGuard dg(w.device());
+  dtg::adagrad_apply(w.data_ptr<float>(), opt_ptr<bf16_t>(mirror), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                     acc.data_ptr<float>(), w.numel(), hyper.data_ptr<float>(), (float)eps, (float)gscale, zero_grad,
+                     cur_stream());
+}
+
+void adam_apply(Tensor w, c10::optional<Tensor> mirror, Tensor g, Tensor m, Tensor v, Tensor hyper, double b1,
+                double b2, double eps, double wd, double gscale, bool zero_grad) {
+  check_flat(w, g, mirror);
+  check_state(m, w);
+  check_state(v, w);
+  check_hyper(hyper);
+  c10::DeviceGuard dg(w.device());
+  dtg::adam_apply(w.data_ptr<float>(), opt_ptr<bf16_t>(mirror), g.data_ptr(), g.scalar_type() == at::kBFloat16,
+                  m.data_ptr<float>(), v.data_ptr<float>(), w.numel(), hyper.data_ptr<float>(), (float)b1, (float)b2,
+                  (float)eps, (float)wd, (float)gscale, zero_grad, cur_stream());
+}
+
+void axpby(Tensor acc, Tensor g, double alpha, double beta) {
+  CHECK_IN(acc);
+  CHECK_IN(g);
+  CHECK_DT(acc, at::kFloat);
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "g must be fp32 or bf16");
+  TORCH_CHECK(acc.numel() == g.numel(), "size mismatch");
+  c10::DeviceGuard dg(acc.device());
+  dtg::axpby(acc.data_ptr<float>(), g.data_ptr(), g.scalar_type() == at::kBFloat16, acc.numel(), (float)alpha,
+             (float)beta, cur_stream());
+}
+
+void f32_to_bf16(Tensor x, Tensor y) {
+  CHECK_IN(x);
+  CHECK_IN(y);
+  CHECK_DT(x, at::kFloat);
+  CHECK_DT(y, at::kBFloat16);
+  TORCH_CHECK(x.numel() == y.numel(), "size mismatch");
+  c10::DeviceGuard dg(x.device());
+  dtg::f32_to_bf16(x.data_ptr<float>(), bfp(y), x.numel(), cur_stream());
+}
+
+// ---- batchnorm -------------------------------------------------------------------------------
+// x: NHWC-contiguous bf16 viewed as [M, C] (the caller passes channels_last tensors flattened).
+std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta,
+                                                Tensor rmean, Tensor rvar, double momentum, double eps, bool relu) {
+  CHECK_IN(x);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2, "x must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  if (res.has_value() && res->defined()) {
+    CHECK_IN(*res);
+    CHECK_DT(*res, at::kBFloat16);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt);
+  auto ws = at::empty({dtg::bn_workspace_floats(M, C)}, fopt);
+  dtg::bn_fwd_train(cbfp(x), res.has_value() && res->defined() ? cbfp(*res) : nullptr, bfp(y),
+                    gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                    smean.data_ptr<float>(), sinv.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)momentum,
+                    (float)eps, relu, cur_stream());
+  return {y, smean, sinv};
+}
+
+Tensor bn_fwd_infer(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
+                    double eps, bool relu) {
+  CHECK_IN(x);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2, "x must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  if (res.has_value() && res->defined()) {
+    CHECK_IN(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty_like(x);
+  auto ws = at::empty({2LL * C}, x.options().dtype(at::kFloat));
+  dtg::bn_fwd_infer(cbfp(x), res.has_value() && res->defined() ? cbfp(*res) : nullptr, bfp(y),
+                    gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                    ws.data_ptr<float>(), M, C, (float)eps, relu, cur_stream());
+  return y;
+}
+
+std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x,
+                                                                  Tensor gamma, Tensor smean, Tensor sinv, bool relu,
+                                                                  bool want_dres) {
+  CHECK_IN(dy);
+  CHECK_IN(x);
+  CHECK_DT(dy, at::kBFloat16);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(dy.sizes() == x.sizes() && x.dim() == 2, "dy/x must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
+    CHECK_IN(*y);
+    TORCH_CHECK(y->sizes() == x.sizes(), "y shape mismatch");
+  }
+  for (const Tensor* t : {&gamma, &smean, &sinv}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto dx = at::empty_like(x);
+  c10::optional<Tensor> dres;
+  if (want_dres) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  auto ws = at::empty({dtg::bn_workspace_floats(M, C) + C}, fopt);
+  dtg::bn_bwd(cbfp(dy), relu ? cbfp(*y) : nullptr, cbfp(x), gamma.data_ptr<float>(), smean.data_ptr<float>(),
+              sinv.data_ptr<float>(), bfp(dx), want_dres ? bfp(*dres) : nullptr, dgamma.data_ptr<float>(),
+              dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu, cur_stream());
+  return {dx, dres, dgamma, dbeta};
+}
+
+// ---- softmax cross entropy -----------------------------------------------------------------
+std::tuple<Tensor, c10::optional<Tensor>, Tensor> softmax_xent(Tensor logits, Tensor labels, double scale,
+                                                                bool want_grad) {
+  CHECK_IN(logits);
+  CHECK_IN(labels);
+  TORCH_CHECK(logits.dim() == 2, "logits must be [B, V]");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/fp32");
+  CHECK_DT(labels, at::kLong);
+  TORCH_CHECK(labels.numel() == logits.size(0), "labels size mismatch");
+  c10::DeviceGuard dg(logits.device());
+  const long long B = logits.size(0);
+  const int V = (int)logits.size(1);
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({B}, fopt), lse = at::empty({B}, fopt);
+  c10::optional<Tensor> dx;
+  if (want_grad) dx = at::empty_like(logits);
+  if (B > 0)
+    dtg::softmax_xent(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), B, V,
+                      (float)scale, loss.data_ptr<float>(), want_grad ? dx->data_ptr() : nullptr,
+                      lse.data_ptr<float>(), cur_stream());
+  return {loss, dx, lse};
+}
+
+// ---- GEMM ----------------------------------------------------------------------------------
+// out[M,N] = act(alpha * op(A) op(B) + beta*out + bias).  a_kc: A stored [M,K] (else [K,M]);
+// b_kc: B stored [N,K] (else [K,N]).  Row strides are taken from the 2-D tensors.
+void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, double beta,
+          c10::optional<Tensor> bias, int64_t act, int64_t split_k) {
+  CHECK_CUDA(A);
+  CHECK_CUDA(B);
+  CHECK_CUDA(out);
+  CHECK_DT(A, at::kBFloat16);
+  CHECK_DT(B, at::kBFloat16);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && out.dim() == 2, "gemm operands must be 2-D");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && out.stride(1) == 1, "inner dim must be contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out fp32/bf16");
+  const int M = (int)(a_kc ? A.size(0) : A.size(1));
+  const int K = (int)(a_kc ? A.size(1) : A.size(0));
+  const int N = (int)(b_kc ? B.size(0) : B.size(1));
+  const int Kb = (int)(b_kc ? B.size(1) : B.size(0));
+  TORCH_CHECK(K == Kb, "gemm K mismatch: ", K, " vs ", Kb);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "gemm out shape mismatch");
+  TORCH_CHECK(K % 8 == 0, "gemm needs K % 8 == 0 (pad the reduction dim)");
+  TORCH_CHECK(a_kc || M % 8 == 0, "K-major A needs M % 8 == 0");
+  TORCH_CHECK(b_kc || N % 8 == 0, "K-major B needs N % 8 == 0");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "row strides must be 16-byte multiples");
+  TORCH_CHECK(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0, "16-byte alignment");
+  const float* bptr = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_IN(*bias);
+    CHECK_DT(*bias, at::kFloat);
+    TORCH_CHECK(bias->numel() == N, "bias size mismatch");
+    bptr = bias->data_ptr<float>();
+  }
+  c10::DeviceGuard dg(A.device());
+  int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K);
+  Tensor ws;
+  float* wsp = nullptr;
+  if (sk > 1) {
+    ws = at::empty({dtg::gemm_workspace_floats(M, N, K, sk)}, A.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  dtg::gemm_bf16(cbfp(A), A.stride(0), a_kc, cbfp(B), B.stride(0), b_kc, out.data_ptr(), out.stride(0),
+                 out.scalar_type() == at::kBFloat16, M, N, K, (float)alpha, (float)beta, bptr, (int)act, sk, wsp,
+                 cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "dtg gfx950 HIP kernels";
+  m.def("sgd_apply", &sgd_apply);
+  m.def("momentum_apply", &momentum_apply);
+  m.def("adagrad_apply", &adagrad_apply);
+  m.def("adam_apply", &adam_apply);
+  m.def("axpby", &axpby);
+  m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_infer", &bn_fwd_infer);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("gemm", &gemm);
+}

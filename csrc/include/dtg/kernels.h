@@ -1,0 +1,49 @@
+// Host-side launch API of dtg's HIP kernels.  Raw pointers + hipStream_t only: the torch
+// bindings (csrc/bindings/) validate tensors and pass the current stream, so every launch is
+// stream-ordered and hipGraph-capturable (no allocation, no sync inside).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dtg {
+typedef unsigned short bf16_t;
+
+// ---- optimizer applies over flat buffers (optim.hip) -------------------------------------------
+// hyper: device float[2] = {lr, step}
+void sgd_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, long long n, const float* hyper, float wd,
+               float gscale, int zero_grad, hipStream_t st);
+void momentum_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* mom, long long n,
+                    const float* hyper, float mu, float wd, int nesterov, float gscale, int zero_grad,
+                    hipStream_t st);
+void adagrad_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* acc, long long n,
+                   const float* hyper, float eps, float gscale, int zero_grad, hipStream_t st);
+void adam_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* m, float* v, long long n,
+                const float* hyper, float b1, float b2, float eps, float wd, float gscale, int zero_grad,
+                hipStream_t st);
+void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st);
+void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
+
+// ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
+long long bn_workspace_floats(long long M, int C);
+void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                  float* rmean, float* rvar, float* smean, float* sinv, float* ws, long long M, int C,
+                  float momentum, float eps, int relu, hipStream_t st);
+void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                  const float* rmean, const float* rvar, float* ws, long long M, int C, float eps, int relu,
+                  hipStream_t st);
+void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gamma, const float* smean,
+            const float* sinv, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M, int C,
+            int relu, hipStream_t st);
+
+// ---- softmax cross-entropy (softmax_xent.hip) ------------------------------------------------
+void softmax_xent(const void* x, int x_bf16, const long long* label, long long B, int V, float scale, float* loss,
+                  void* dx, float* lse, hipStream_t st);
+
+// ---- GEMM (gemm.hip) -------------------------------------------------------------------------
+long long gemm_workspace_floats(int M, int N, int K, int split_k);
+int gemm_pick_split(int M, int N, int K);
+void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
+               long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
+               int split_k, float* ws, hipStream_t st);
+
+}  // namespace dtg

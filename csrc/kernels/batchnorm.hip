@@ -1,0 +1,351 @@
+// NHWC BatchNorm for training, fused with the residual add and ReLU that follow it in ResNet
+// bottlenecks:   y = relu( (x - mean) * invstd * gamma + beta  [+ residual] )
+//
+// Memory-bound (HBM3E): every pass streams bf16 rows with 16-byte lanes.  A block owns a fixed
+// slab of CW = TPR*8 channels and walks rows, so each lane keeps its 8 channels' scale/shift and
+// partial sums in registers; no per-element channel index arithmetic.  Statistics are fp32 per
+// row-chunk, reduced deterministically (no atomics) in double by a finalize kernel.
+//
+// Passes (training):  fwd = stats(x) -> finalize -> apply(x,res)             3 launches
+//                     bwd = reduce(dy,y,x) -> finalize -> dx(dy,y,x)          3 launches
+// The relu mask in backward comes from the saved output y (which the next conv already keeps
+// alive for its own backward), so no mask tensor is materialised.
+#include "dtg/common.h"
+#include "dtg/kernels.h"
+
+namespace dtg {
+
+static constexpr int kBlk = 256;
+
+struct BnGeom {
+  int tpr;    // threads per row (8 channels each)
+  int cw;     // channels per block slab
+  int gy;     // slabs
+  int nchunk; // row chunks
+  long long rows_per_chunk;
+};
+
+static BnGeom bn_geom(long long M, int C) {
+  BnGeom g;
+  const int cw_need = C < 512 ? C : 512;
+  g.tpr = 8;
+  while (g.tpr * 8 < cw_need && g.tpr < 64) g.tpr *= 2;
+  g.cw = g.tpr * 8;
+  g.gy = (C + g.cw - 1) / g.cw;
+  const int rpp = kBlk / g.tpr;
+  long long max_chunks = (M + rpp - 1) / rpp;
+  long long nc = 1024 / g.gy;
+  if (nc < 1) nc = 1;
+  if (nc > max_chunks) nc = max_chunks;
+  g.rows_per_chunk = (M + nc - 1) / nc;
+  g.nchunk = (int)((M + g.rows_per_chunk - 1) / g.rows_per_chunk);
+  return g;
+}
+
+long long bn_workspace_floats(long long M, int C) {
+  BnGeom g = bn_geom(M, C);
+  return (long long)g.nchunk * 2 * C + 4LL * C;
+}
+
+// ---- pass 1 (fwd): per-chunk sum / sum of squares ------------------------------------------
+template <int TPR>
+__global__ void __launch_bounds__(kBlk) bn_stats_kernel(const bf16_t* __restrict__ x, long long M, int C,
+                                                        long long rpc, float* __restrict__ part) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  __shared__ float sh[2][RPP][CW + 4];
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < C) {
+    long long m = m0 + ty;
+    // 2-deep unroll keeps two 16B loads in flight per lane
+    for (; m + RPP < m1; m += 2 * RPP) {
+      float a[8], b[8];
+      load8_bf16(x + m * C + c0, a);
+      load8_bf16(x + (m + RPP) * C + c0, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += a[k] + b[k]; q[k] += a[k] * a[k] + b[k] * b[k]; }
+    }
+    if (m < m1) {
+      float a[8];
+      load8_bf16(x + m * C + c0, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += a[k]; q[k] += a[k] * a[k]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sh[0][ty][tx * 8 + k] = s[k]; sh[1][ty][tx * 8 + k] = q[k]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < CW; c += kBlk) {
+    float ts = 0.f, tq = 0.f;
+#pragma unroll 4
+    for (int r = 0; r < RPP; ++r) { ts += sh[0][r][c]; tq += sh[1][r][c]; }
+    const int cc = blockIdx.y * CW + c;
+    if (cc < C) {
+      part[((long long)blockIdx.x * 2 + 0) * C + cc] = ts;
+      part[((long long)blockIdx.x * 2 + 1) * C + cc] = tq;
+    }
+  }
+}
+
+// ---- finalize: reduce chunk partials (double), emit per-channel coefficients -----------------
+// mode 0 (fwd):  out0 = scale = gamma*invstd, out1 = shift = beta - mean*scale,
+//                save_mean/save_invstd, running stats update.
+// mode 1 (bwd):  a = gamma*invstd; dgamma = sum(dp*xhat), dbeta = sum(dp);
+//                dx = a*dp + bx*x + c0   with bx = -a*invstd*dgamma/M, c0 = -a*dbeta/M - bx*mean
+__global__ void __launch_bounds__(kBlk) bn_finalize_kernel(const float* __restrict__ part, int nchunk, long long M,
+                                                           int C, int mode, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* __restrict__ rmean,
+                                                           float* __restrict__ rvar, float* __restrict__ smean,
+                                                           float* __restrict__ sinv, float momentum, float eps,
+                                                           float* __restrict__ coef, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta) {
+  __shared__ double sh[2][4][64];
+  const int cl = threadIdx.x % 64, r = threadIdx.x / 64;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int k = r; k < nchunk; k += 4) {
+      s += (double)part[((long long)k * 2 + 0) * C + c];
+      q += (double)part[((long long)k * 2 + 1) * C + c];
+    }
+  }
+  sh[0][r][cl] = s;
+  sh[1][r][cl] = q;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  s = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+  q = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  const double invM = 1.0 / (double)M;
+  const float g = gamma ? gamma[c] : 1.f;
+  if (mode == 0) {
+    const double mean = s * invM;
+    double var = q * invM - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = g * invstd;
+    coef[c] = sc;
+    coef[C + c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
+    if (smean) smean[c] = (float)mean;
+    if (sinv) sinv[c] = invstd;
+    if (rmean) rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    if (rvar) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  } else {
+    // s = sum(dp), q = sum(dp * xhat)
+    const float mean = smean[c], invstd = sinv[c];
+    const float a = g * invstd;
+    const float bx = (float)(-(double)a * invstd * q * invM);
+    const float c0 = (float)(-(double)a * s * invM) - bx * mean;
+    coef[c] = a;
+    coef[C + c] = bx;
+    coef[2 * C + c] = c0;
+    if (dgamma) dgamma[c] = (float)q;
+    if (dbeta) dbeta[c] = (float)s;
+  }
+}
+
+// ---- pass 2 (fwd): apply scale/shift (+residual) (+relu) -------------------------------------
+template <int TPR, bool RES, bool RELU>
+__global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                        bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                        long long M, int C, long long rpc) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  if (c0 >= C) return;
+  float sc[8], sf[8];
+  load8_f32(coef + c0, sc);
+  load8_f32(coef + C + c0, sf);
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  for (long long m = m0 + ty; m < m1; m += RPP) {
+    const long long off = m * C + c0;
+    float a[8];
+    load8_bf16(x + off, a);
+    float r[8];
+    if constexpr (RES) load8_bf16(res + off, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = a[k] * sc[k] + sf[k];
+      if constexpr (RES) v += r[k];
+      if constexpr (RELU) v = fmaxf(v, 0.f);
+      a[k] = v;
+    }
+    store8_bf16(y + off, a);
+  }
+}
+
+// ---- pass 1 (bwd): sum(dp), sum(dp*xhat), dp = dy * [y>0] -----------------------------------
+template <int TPR, bool RELU>
+__global__ void __launch_bounds__(kBlk) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ y,
+                                                             const bf16_t* __restrict__ x,
+                                                             const float* __restrict__ smean,
+                                                             const float* __restrict__ sinv, long long M, int C,
+                                                             long long rpc, float* __restrict__ part) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  __shared__ float sh[2][RPP][CW + 4];
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < C) {
+    float mu[8], is[8];
+    load8_f32(smean + c0, mu);
+    load8_f32(sinv + c0, is);
+    const long long m0 = (long long)blockIdx.x * rpc;
+    const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+    for (long long m = m0 + ty; m < m1; m += RPP) {
+      const long long off = m * C + c0;
+      float g[8], xv[8];
+      load8_bf16(dy + off, g);
+      load8_bf16(x + off, xv);
+      if constexpr (RELU) {
+        float yv[8];
+        load8_bf16(y + off, yv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sh[0][ty][tx * 8 + k] = s[k]; sh[1][ty][tx * 8 + k] = q[k]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < CW; c += kBlk) {
+    float ts = 0.f, tq = 0.f;
+#pragma unroll 4
+    for (int r = 0; r < RPP; ++r) { ts += sh[0][r][c]; tq += sh[1][r][c]; }
+    const int cc = blockIdx.y * CW + c;
+    if (cc < C) {
+      part[((long long)blockIdx.x * 2 + 0) * C + cc] = ts;
+      part[((long long)blockIdx.x * 2 + 1) * C + cc] = tq;
+    }
+  }
+}
+
+// ---- pass 2 (bwd): dx = a*dp + bx*x + c0 ; dres = dp ------------------------------------------
+template <int TPR, bool RELU, bool DRES>
+__global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                         const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                                         bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+                                                         long long M, int C, long long rpc) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  if (c0 >= C) return;
+  float a[8], bx[8], cc[8];
+  load8_f32(coef + c0, a);
+  load8_f32(coef + C + c0, bx);
+  load8_f32(coef + 2 * C + c0, cc);
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  for (long long m = m0 + ty; m < m1; m += RPP) {
+    const long long off = m * C + c0;
+    float g[8], xv[8];
+    load8_bf16(dy + off, g);
+    load8_bf16(x + off, xv);
+    if constexpr (RELU) {
+      float yv[8];
+      load8_bf16(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if constexpr (DRES) store8_bf16(dres + off, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = a[k] * g[k] + bx[k] * xv[k] + cc[k];
+    store8_bf16(dx + off, o);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+#define DTG_TPR_SWITCH(tpr, ...)                       \
+  switch (tpr) {                                       \
+    case 8: { constexpr int T = 8; __VA_ARGS__; } break;   \
+    case 16: { constexpr int T = 16; __VA_ARGS__; } break; \
+    case 32: { constexpr int T = 32; __VA_ARGS__; } break; \
+    default: { constexpr int T = 64; __VA_ARGS__; } break; \
+  }
+
+void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                  float* rmean, float* rvar, float* smean, float* sinv, float* ws, long long M, int C,
+                  float momentum, float eps, int relu, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  float* part = ws;
+  float* coef = ws + (long long)g.nchunk * 2 * C;
+  dim3 grid(g.nchunk, g.gy);
+  DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
+  bn_finalize_kernel<<<(C + 63) / 64, kBlk, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
+                                                    momentum, eps, coef, nullptr, nullptr);
+  DTG_TPR_SWITCH(g.tpr, {
+    if (res) {
+      if (relu) bn_apply_kernel<T, true, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      else bn_apply_kernel<T, true, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+    } else {
+      if (relu) bn_apply_kernel<T, false, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      else bn_apply_kernel<T, false, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+    }
+  });
+}
+
+// Inference: coefficients from running statistics (tiny launch) then the same apply pass.
+__global__ void bn_infer_coef_kernel(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                     float eps, int C, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rvar[c] + eps);
+  const float sc = (gamma ? gamma[c] : 1.f) * inv;
+  coef[c] = sc;
+  coef[C + c] = (beta ? beta[c] : 0.f) - rmean[c] * sc;
+}
+
+void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                  const float* rmean, const float* rvar, float* ws, long long M, int C, float eps, int relu,
+                  hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  float* coef = ws;
+  bn_infer_coef_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, rmean, rvar, eps, C, coef);
+  dim3 grid(g.nchunk, g.gy);
+  DTG_TPR_SWITCH(g.tpr, {
+    if (res) {
+      if (relu) bn_apply_kernel<T, true, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      else bn_apply_kernel<T, true, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+    } else {
+      if (relu) bn_apply_kernel<T, false, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      else bn_apply_kernel<T, false, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+    }
+  });
+}
+
+void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gamma, const float* smean,
+            const float* sinv, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M, int C,
+            int relu, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  float* part = ws;
+  float* coef = ws + (long long)g.nchunk * 2 * C;
+  dim3 grid(g.nchunk, g.gy);
+  DTG_TPR_SWITCH(g.tpr, {
+    if (relu) bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
+    else bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
+  });
+  bn_finalize_kernel<<<(C + 63) / 64, kBlk, 0, st>>>(part, g.nchunk, M, C, 1, gamma, nullptr, nullptr, nullptr,
+                                                    const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
+                                                    coef, dgamma, dbeta);
+  DTG_TPR_SWITCH(g.tpr, {
+    if (relu) {
+      if (dres) bn_bwd_dx_kernel<T, true, true><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+      else bn_bwd_dx_kernel<T, true, false><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+    } else {
+      if (dres) bn_bwd_dx_kernel<T, false, true><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+      else bn_bwd_dx_kernel<T, false, false><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+    }
+  });
+}
+
+}  // namespace dtg

@@ -1,0 +1,2 @@
+"""Model zoo: toy linear problem (reference parity), MNIST CNN, ResNet-50, BERT-base."""
+from .resnet import resnet50, ResNet, synthetic_batch  # noqa: F401

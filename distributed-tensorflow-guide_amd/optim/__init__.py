@@ -1,0 +1,2 @@
+"""Optimizers: fused flat-buffer applies (north-star models)."""
+from .fused import FusedSGD, FusedAdam, FusedAdagrad  # noqa: F401

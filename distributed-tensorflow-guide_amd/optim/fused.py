@@ -1,0 +1,90 @@
+"""Fused flat-buffer optimizers for the north-star models (one kernel launch per dtype group).
+
+The per-step hyper-parameters (learning rate, step count) live in a device tensor so a whole
+training step can be captured in a hipGraph and replayed with a new schedule value.
+"""
+import torch
+
+from ..ops import optim_kernels as K
+
+
+class _FlatOptimizer:
+    def __init__(self, flat, lr, weight_decay=0.0, wd_groups=("compute",)):
+        self.flat = flat
+        groups = list(flat)
+        dev = groups[0].master.device if groups else torch.device("cpu")
+        self.hyper = torch.tensor([float(lr), 0.0], dtype=torch.float32, device=dev)
+        self.lr = float(lr)
+        self.weight_decay = weight_decay
+        self.wd_groups = set(wd_groups)
+        self.step_count = 0
+
+    def set_lr(self, lr):
+        self.lr = float(lr)
+        self.hyper[0].fill_(self.lr)
+
+    def _wd(self, g):
+        return self.weight_decay if g.name in self.wd_groups else 0.0
+
+    def step(self, grad_scale=1.0, zero_grad=True):
+        self.step_count += 1
+        self.hyper[1].add_(1.0)
+        for g in self.flat:
+            self._apply(g, grad_scale, zero_grad)
+
+    def state_dict(self):
+        return {"step": self.step_count, "lr": self.lr,
+                "state": {g.name: {k: v for k, v in g.state.items()} for g in self.flat}}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd.get("step", 0))
+        self.set_lr(sd.get("lr", self.lr))
+        self.hyper[1].fill_(float(self.step_count))
+        for g in self.flat:
+            for k, v in sd.get("state", {}).get(g.name, {}).items():
+                g.state_buffer(k).copy_(v)
+
+
+class FusedSGD(_FlatOptimizer):
+    """Momentum SGD (PyTorch semantics, optional Nesterov); momentum=0 -> plain SGD."""
+
+    def __init__(self, flat, lr, momentum=0.9, weight_decay=0.0, nesterov=False, wd_groups=("compute",)):
+        super().__init__(flat, lr, weight_decay, wd_groups)
+        self.momentum = momentum
+        self.nesterov = nesterov
+
+    def _apply(self, g, gscale, zero_grad):
+        if self.momentum == 0.0:
+            K.sgd(g.master, g.grad, self.hyper, g.mirror, self._wd(g), gscale, zero_grad)
+        else:
+            K.momentum(g.master, g.grad, g.state_buffer("momentum"), self.hyper, g.mirror, self.momentum,
+                       self._wd(g), self.nesterov, gscale, zero_grad)
+
+
+class FusedAdam(_FlatOptimizer):
+    """AdamW with decoupled weight decay (BERT pre-training)."""
+
+    def __init__(self, flat, lr, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.01, wd_groups=("compute",)):
+        super().__init__(flat, lr, weight_decay, wd_groups)
+        self.betas = betas
+        self.eps = eps
+
+    def _apply(self, g, gscale, zero_grad):
+        K.adam(g.master, g.grad, g.state_buffer("m"), g.state_buffer("v"), self.hyper, g.mirror, self.betas[0],
+               self.betas[1], self.eps, self._wd(g), gscale, zero_grad)
+
+
+class FusedAdagrad(_FlatOptimizer):
+    """TF-style Adagrad (initial accumulator 0.1, no epsilon) -- DOWNPOUR's optimizer."""
+
+    def __init__(self, flat, lr, initial_accumulator_value=0.1, eps=0.0):
+        super().__init__(flat, lr, 0.0)
+        self.init_acc = initial_accumulator_value
+        self.eps = eps
+
+    def _apply(self, g, gscale, zero_grad):
+        fresh = "acc" not in g.state
+        acc = g.state_buffer("acc")
+        if fresh:
+            acc.fill_(self.init_acc)
+        K.adagrad(g.master, g.grad, acc, self.hyper, g.mirror, self.eps, gscale, zero_grad)

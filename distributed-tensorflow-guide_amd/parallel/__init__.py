@@ -1,0 +1,4 @@
+"""Parallelism: flat parameter buffers, RCCL all-reduce DP, process-group bootstrap."""
+from .flat import FlatParams, FlatGroup  # noqa: F401
+from .ddp import DataParallel  # noqa: F401
+from . import comm  # noqa: F401

@@ -1,0 +1,58 @@
+"""Process-group bootstrap: one process per GPU, RCCL ("nccl" backend on ROCm) over xGMI, or gloo
+on CPU.  Ranks come from the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*)
+or from a :class:`dtg.ClusterSpec` (job "worker", task_index = rank).
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), int(
+        os.environ.get("WORLD_SIZE", "1"))
+
+
+def init(backend=None, timeout_s=600):
+    """Initialise the default process group from the environment (no-op for world_size 1).
+
+    Returns (rank, local_rank, world, device)."""
+    rank, local, world = env_rank()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, local, world, device
+
+
+def barrier():
+    if dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float, device):
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,115 @@
+"""Synchronous data parallelism: bucketed RCCL all-reduce overlapped with backward.
+
+This is the fast path of ``SyncReplicasOptimizer`` (replicas_to_aggregate == total_num_replicas,
+no PS) and the BASELINE north-star config ("ResNet-50 bf16 sync all-reduce DP
+on 8x MI355X").  One process per GPU, ``torch.distributed`` backend "nccl" (= RCCL on ROCm) over
+xGMI; "gloo" for CPU tests.
+
+Design:
+* gradients live in the flat buffers of :class:`FlatParams`; a bucket is a contiguous slice of a
+  group's flat grad buffer (no flatten copies) -- the buffer is laid out in backward order;
+* a post-accumulate-grad hook per parameter counts down its bucket; when the last gradient of a
+  bucket lands, its all-reduce (SUM) is issued asynchronously.  RCCL runs on its own stream and
+  waits on the compute stream's event at launch, so it overlaps the rest of backward;
+* ``finish()`` joins all outstanding collectives into the compute stream; the 1/world averaging is
+  folded into the optimizer's gradient scale (no separate divide kernel);
+* bucket size default 32 MB: large enough to amortise the ~tens-of-µs RCCL launch against the
+  ~1 TB/s aggregate xGMI rate, small enough that ResNet-50's 51 MB of bf16 gradients forms 2
+  buckets that start before backward ends (sweep with ``bucket_mb``).
+"""
+import torch
+import torch.distributed as dist
+
+
+class _Bucket:
+    __slots__ = ("group", "start", "end", "params", "pending", "work", "index")
+
+    def __init__(self, group, start, index):
+        self.group = group
+        self.start = start
+        self.end = start
+        self.params = []
+        self.pending = 0
+        self.work = None
+        self.index = index
+
+    def view(self):
+        return self.group.grad[self.start:self.end]
+
+
+class DataParallel:
+    def __init__(self, flat, process_group=None, bucket_mb=32.0, overlap=True):
+        self.flat = flat
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.overlap = overlap and self.world > 1
+        self.buckets = []
+        self._hooks = []
+        cap = int(bucket_mb * (1 << 20))
+        for g in flat:
+            esz = g.grad.element_size()
+            b = None
+            for i, (name, p, off, n) in enumerate(g.param_slices()):
+                if b is None or (b.end - b.start) * esz >= cap:
+                    b = _Bucket(g, off, len(self.buckets))
+                    self.buckets.append(b)
+                b.params.append(p)
+                nxt = g.offsets[i + 1] if i + 1 < len(g.offsets) else g.numel
+                b.end = nxt
+        self._param_bucket = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._param_bucket[p] = b
+        if self.overlap:
+            for p in self._param_bucket:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self._reset()
+
+    # -- hooks ---------------------------------------------------------------------------------
+    def _reset(self):
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+
+    def _launch(self, b):
+        b.work = dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def _on_grad(self, p):
+        b = self._param_bucket[p]
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    # -- step ------------------------------------------------------------------------------------
+    @property
+    def grad_scale(self):
+        """Factor the optimizer applies to the summed gradients (1/world: mean)."""
+        return 1.0 / self.world
+
+    def finish(self):
+        """Wait for every bucket's all-reduce (launching any that did not fire)."""
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            if b.work is None:
+                self._launch(b)
+        for b in self.buckets:
+            b.work.wait()
+        self._reset()
+
+    def broadcast_parameters(self, src=0):
+        """Chief broadcast of initial weights and module buffers (replaces the reference's
+        ``assign_global`` + ``sleep(10)`` bootstrap, DOWNPOUR/DOWNPOUR.py:129-135)."""
+        if self.world == 1:
+            return
+        for g in self.flat:
+            dist.broadcast(g.master, src, group=self.pg)
+            g.refresh_mirror()
+        for buf in self.flat.module.buffers():
+            if buf.is_floating_point() or buf.dtype in (torch.int64, torch.int32):
+                dist.broadcast(buf, src, group=self.pg)
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

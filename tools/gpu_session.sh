@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session: tests, benchmark, profile.  Every GPU step has its own time limit; a
+# crash/fault/timeout (exit >= 124 or signal) stops the session so nothing else touches the GPU.
+# Usage: tools/gpu_session.sh [steps...]   steps: test bench bench_miopen prof smoke
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+STEPS=${*:-"test bench prof"}
+
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/session.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/session.log
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "fatal rc=$rc in $name: stopping session"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    test) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
+            python3 bench.py --steps 5 --warmup 3 ;;
+    *) run "$s" 900 bash -c "$s" ;;
+  esac
+done
