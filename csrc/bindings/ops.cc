@@ -253,7 +253,7 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
   const int Kb = (int)(b_kc ? B.size(1) : B.size(0));
   TORCH_CHECK(K == Kb, "gemm K mismatch: ", K, " vs ", Kb);
   TORCH_CHECK(out.size(0) == M && out.size(1) == N, "gemm out shape mismatch");
-  TORCH_CHECK(K % 8 == 0, "gemm needs K % 8 == 0 (pad the reduction dim)");
+  TORCH_CHECK(K % 8 == 0 || (!a_kc && !b_kc), "K-contiguous operands need K % 8 == 0 (pad the reduction dim)");
   TORCH_CHECK(a_kc || M % 8 == 0, "K-major A needs M % 8 == 0");
   TORCH_CHECK(b_kc || N % 8 == 0, "K-major B needs N % 8 == 0");
   TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "row strides must be 16-byte multiples");

@@ -2,15 +2,17 @@
 //
 //   C[M,N] (+)= A[M,K] * B[K,N]        bf16 inputs, fp32 accumulate (v_mfma_f32_16x16x32_bf16)
 //
-// Tiling: 256 threads = 4 waves (2x2), block tile BM x BN x BK = 128 x 128 x 64, each wave owns a
-// 64x64 sub-tile = 4x4 MFMA 16x16 accumulators (64 acc VGPRs).  Operand tiles are staged HBM->LDS
-// with global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction, no VGPR round trip) into a
-// 2-deep LDS ring (64 KiB: 2 blocks/CU), one barrier per K-step.
+// Tiling: 256 threads = 4 waves; each wave owns a 64x64 output sub-tile = 4x4 MFMA 16x16
+// accumulators (64 acc VGPRs).  Block tile BM x BN x 64 with (BM/64) x (BN/64) = 4 waves:
+//   Cfg<128,128>  2x2 waves  -- general
+//   Cfg<256, 64>  4x1 waves  -- skinny N (64-channel convs): A streamed once, no wasted MFMAs
+// Operand tiles are staged HBM->LDS with global_load_lds_dwordx4 (LDS-DMA, 1 KiB per
+// wave-instruction, no VGPR round trip) into a 2-deep LDS ring, one barrier per K-step.
 //
 // Each operand is either
 //   KC  ("K-contiguous")  : element (row, k) at base(row) + k          -> LDS [rows][64]  128 B rows,
-//        16-B chunk XOR-swizzled by (row & 7); fragments by ds_read_b128
-//   MC  ("MN-contiguous") : element (k, col) at base(k) + col          -> LDS [64][rows]  256 B rows,
+//        16-B chunk XOR-swizzled by (row & 7); fragments by ds_read_b128 (conflict-free)
+//   MC  ("MN-contiguous") : element (k, col) at base(k) + col          -> LDS [64][rows]  2*rows B rows,
 //        16-B chunk XOR-swizzled by 2*f(k); fragments by 2x ds_read_b64_tr_b16 (hardware transpose)
 // so the three training GEMMs (fwd X*W^T, dgrad dY*W, wgrad dY^T*X) all run without explicit
 // transposes.  With LDS-DMA the destination is lane-linear, so the swizzle is applied to the
@@ -30,19 +32,32 @@ typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) v4bf lds_v4bf;
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BK = 64;
 constexpr int NT = 256;
-constexpr int TILE_BYTES = 128 * 64 * 2;               // 16 KiB per operand per stage
-constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;          // 2 operands x 2 stages
+
+template <int BM_, int BN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int WM = BM / 64, WN = BN / 64;
+  static_assert(WM * WN == 4, "4 waves of 64x64");
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+  // epilogue staging: 64 rows x (BN+4) fp32 must fit in the (then idle) operand ring
+  static_assert(64 * (BN + 4) * 4 <= LDS_BYTES, "epilogue staging does not fit");
+};
 
 // 16-byte zero page in global memory for out-of-range chunks (glds needs a global source).
 __device__ __attribute__((aligned(64))) static const bf16_t g_zero_page[32] = {0};
 
 __device__ __forceinline__ const void* zero_src() { return (const void*)g_zero_page; }
 
-// swizzle of the 16-B chunk index (0..15) of a 256-B MC row; keeps 32-B pairs together and makes
-// the 8 rows read by one ds_read_b64_tr_b16 half-wave distinct (conflict-free)
-__device__ __forceinline__ int mc_swz(int k) { return (((k & 3) | (((k >> 3) & 1) << 2)) << 1); }
+// swizzle of the 16-B chunk index of an MC row (CH chunks): keeps 32-B pairs together and makes
+// the 8 rows read by one ds_read_b64_tr_b16 half-wave distinct where the row is wide enough
+template <int CH>
+__device__ __forceinline__ int mc_swz(int k) {
+  return ((((k & 3) | (((k >> 3) & 1) << 2)) << 1) & (CH - 1));
+}
 
 // ---- dense sources -------------------------------------------------------------------------
 // KC: matrix stored [rows][ld] with k contiguous
@@ -68,12 +83,13 @@ struct DenseMC {
 };
 
 // ---- staging ---------------------------------------------------------------------------------
-// KC tile: 128 rows x 64 k; wave-instruction i covers 8 rows; 16 instructions per tile, 4 per wave
-template <class Src>
+// KC tile: ROWS x 64 k (128 B rows); a wave-instruction covers 8 rows
+template <int ROWS, class Src>
 __device__ __forceinline__ void stage_kc(const Src& src, char* lds_tile, int row0, int k0, int wave, int lane) {
+  constexpr int PER_WAVE = ROWS / 32;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r0 = (wave * 4 + i) * 8;
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int r0 = (wave * PER_WAVE + i) * 8;
     const int r = r0 + (lane >> 3);
     const int cl = lane & 7;           // linear chunk position in LDS
     const int c = cl ^ (r & 7);        // source chunk that belongs there
@@ -82,17 +98,20 @@ __device__ __forceinline__ void stage_kc(const Src& src, char* lds_tile, int row
   }
 }
 
-// MC tile: 64 k-rows x 128 cols; wave-instruction covers 4 k-rows; 16 per tile, 4 per wave
-template <class Src>
+// MC tile: 64 k-rows x ROWS cols (2*ROWS B rows); a wave-instruction covers 512/ROWS k-rows
+template <int ROWS, class Src>
 __device__ __forceinline__ void stage_mc(const Src& src, char* lds_tile, int col0, int k0, int wave, int lane) {
+  constexpr int CH = ROWS / 8;          // 16-B chunks per k-row
+  constexpr int KPI = 64 / CH;          // k-rows per wave-instruction
+  constexpr int PER_WAVE = 64 / KPI / 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int kr0 = (wave * 4 + i) * 4;
-    const int kr = kr0 + (lane >> 4);
-    const int cl = lane & 15;
-    const int c = cl ^ mc_swz(kr);
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int kr0 = (wave * PER_WAVE + i) * KPI;
+    const int kr = kr0 + lane / CH;
+    const int cl = lane % CH;
+    const int c = cl ^ mc_swz<CH>(kr);
     const void* g = src.chunk(k0 + kr, col0 + c * 8);
-    __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_tile + kr0 * 256), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_tile + kr0 * ROWS * 2), 16, 0, 0);
   }
 }
 
@@ -104,52 +123,54 @@ __device__ __forceinline__ v8bf frag_kc(const char* lds_tile, int r0, int ks, in
   return *reinterpret_cast<const v8bf*>(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
 }
 
+template <int ROWS>
 __device__ __forceinline__ v8bf frag_mc(const char* lds_tile, int r0, int ks, int lane) {
+  constexpr int CH = ROWS / 8;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int kA = ks * 32 + 8 * g + q;   // rows for elements 0..3
   const int kB = kA + 4;                // rows for elements 4..7
   const int ch = (r0 >> 3) + (p >> 1);  // 16-B chunk of columns r0+4p .. r0+4p+3
   const int sub = (p & 1) * 8;
-  const char* a = lds_tile + kA * 256 + ((ch ^ mc_swz(kA)) << 4) + sub;
-  const char* b = lds_tile + kB * 256 + ((ch ^ mc_swz(kB)) << 4) + sub;
+  const char* a = lds_tile + kA * ROWS * 2 + ((ch ^ mc_swz<CH>(kA)) << 4) + sub;
+  const char* b = lds_tile + kB * ROWS * 2 + ((ch ^ mc_swz<CH>(kB)) << 4) + sub;
   const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(a));
   const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(b));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <bool KC>
+template <bool KC, int ROWS>
 __device__ __forceinline__ v8bf frag(const char* t, int r0, int ks, int lane) {
   if constexpr (KC) return frag_kc(t, r0, ks, lane);
-  else return frag_mc(t, r0, ks, lane);
+  else return frag_mc<ROWS>(t, r0, ks, lane);
 }
 
-template <bool KC, class Src>
+template <bool KC, int ROWS, class Src>
 __device__ __forceinline__ void stage(const Src& s, char* t, int rc0, int k0, int wave, int lane) {
-  if constexpr (KC) stage_kc(s, t, rc0, k0, wave, lane);
-  else stage_mc(s, t, rc0, k0, wave, lane);
+  if constexpr (KC) stage_kc<ROWS>(s, t, rc0, k0, wave, lane);
+  else stage_mc<ROWS>(s, t, rc0, k0, wave, lane);
 }
 
 // ---- main loop -------------------------------------------------------------------------------
-// Accumulates the K range [kbeg, kend) of tile (bm, bn) into acc[4][4].
-template <bool AKC, bool BKC, class SA, class SB>
+// Accumulates the K range [kbeg, kend) of tile (bm0, bn0) into acc[4][4].
+template <class C, bool AKC, bool BKC, class SA, class SB>
 __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, char* smem, int bm0, int bn0, int kbeg, int kend,
                                          f32x4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  char* As[2] = {smem, smem + TILE_BYTES};
-  char* Bs[2] = {smem + 2 * TILE_BYTES, smem + 3 * TILE_BYTES};
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  char* As[2] = {smem, smem + C::STAGE_BYTES};
+  char* Bs[2] = {smem + C::A_BYTES, smem + C::STAGE_BYTES + C::A_BYTES};
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk <= 0) return;
-  stage<AKC>(sa, As[0], bm0, kbeg, wave, lane);
-  stage<BKC>(sb, Bs[0], bn0, kbeg, wave, lane);
+  stage<AKC, C::BM>(sa, As[0], bm0, kbeg, wave, lane);
+  stage<BKC, C::BN>(sb, Bs[0], bn0, kbeg, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      stage<AKC>(sa, As[cur ^ 1], bm0, kbeg + (kt + 1) * BK, wave, lane);
-      stage<BKC>(sb, Bs[cur ^ 1], bn0, kbeg + (kt + 1) * BK, wave, lane);
+      stage<AKC, C::BM>(sa, As[cur ^ 1], bm0, kbeg + (kt + 1) * BK, wave, lane);
+      stage<BKC, C::BN>(sb, Bs[cur ^ 1], bn0, kbeg + (kt + 1) * BK, wave, lane);
     }
     const char* At = As[cur];
     const char* Bt = Bs[cur];
@@ -157,15 +178,55 @@ __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, char* smem,
     for (int ks = 0; ks < 2; ++ks) {
       v8bf a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag<AKC>(At, wm * 64 + i * 16, ks, lane);
+      for (int i = 0; i < 4; ++i) a[i] = frag<AKC, C::BM>(At, wm * 64 + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = frag<BKC>(Bt, wn * 64 + j * 16, ks, lane);
+      for (int j = 0; j < 4; ++j) b[j] = frag<BKC, C::BN>(Bt, wn * 64 + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
+// ---- epilogue ----------------------------------------------------------------------------------
+// Stages the block's fp32 accumulators through LDS (64 rows at a time) so that every global
+// store is a coalesced 16-byte vector; OP(row, col0, float (&v)[8]) finishes 8 consecutive
+// columns (bias, residual/beta, activation, dtype) and stores them.
+template <class C, class OP>
+__device__ __forceinline__ void epilogue_staged(char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+                                                const OP& op) {
+  constexpr int LD = C::BN + 4;  // fp32 row pitch (pad breaks bank aliasing of the column writes)
+  float* st = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  __syncthreads();  // operand ring no longer read by anyone
+#pragma unroll
+  for (int pass = 0; pass < C::WM; ++pass) {
+    if (wm == pass) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    constexpr int CPR = C::BN / 8;  // 8-column groups per row
+    for (int idx = tid; idx < 64 * CPR; idx += NT) {
+      const int rr = idx / CPR, cg = idx % CPR;
+      const int m = bm0 + pass * 64 + rr, n = bn0 + cg * 8;
+      if (m < M && n < N) {
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(st + rr * LD + cg * 8);
+        const float4 b = *reinterpret_cast<const float4*>(st + rr * LD + cg * 8 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        op(m, n, v);
+      }
+    }
     __syncthreads();
   }
 }

@@ -15,7 +15,7 @@
 
 namespace dtg {
 
-static constexpr int kBlk = 256;
+static constexpr int kBlk = 512;   // 8 waves: RPP = 512/TPR rows in flight per block
 
 struct BnGeom {
   int tpr;    // threads per row (8 channels each)
@@ -34,7 +34,8 @@ static BnGeom bn_geom(long long M, int C) {
   g.gy = (C + g.cw - 1) / g.cw;
   const int rpp = kBlk / g.tpr;
   long long max_chunks = (M + rpp - 1) / rpp;
-  long long nc = 1024 / g.gy;
+  // <= 256 row chunks: keeps the finalize reduction short (<= 16 partials per finalize lane)
+  long long nc = 256 / g.gy;
   if (nc < 1) nc = 1;
   if (nc > max_chunks) nc = max_chunks;
   g.rows_per_chunk = (M + nc - 1) / nc;
@@ -95,29 +96,40 @@ __global__ void __launch_bounds__(kBlk) bn_stats_kernel(const bf16_t* __restrict
 //                save_mean/save_invstd, running stats update.
 // mode 1 (bwd):  a = gamma*invstd; dgamma = sum(dp*xhat), dbeta = sum(dp);
 //                dx = a*dp + bx*x + c0   with bx = -a*invstd*dgamma/M, c0 = -a*dbeta/M - bx*mean
-__global__ void __launch_bounds__(kBlk) bn_finalize_kernel(const float* __restrict__ part, int nchunk, long long M,
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ part, int nchunk, long long M,
                                                            int C, int mode, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* __restrict__ rmean,
                                                            float* __restrict__ rvar, float* __restrict__ smean,
                                                            float* __restrict__ sinv, float momentum, float eps,
                                                            float* __restrict__ coef, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta) {
-  __shared__ double sh[2][4][64];
+  constexpr int G = 16;  // chunk groups per channel
+  __shared__ double sh[2][G][64];
   const int cl = threadIdx.x % 64, r = threadIdx.x / 64;
   const int c = blockIdx.x * 64 + cl;
-  double s = 0.0, q = 0.0;
+  float s0 = 0.f, s1 = 0.f, q0 = 0.f, q1 = 0.f;  // two independent chains per sum
   if (c < C) {
-    for (int k = r; k < nchunk; k += 4) {
-      s += (double)part[((long long)k * 2 + 0) * C + c];
-      q += (double)part[((long long)k * 2 + 1) * C + c];
+    int k = r;
+    for (; k + G < nchunk; k += 2 * G) {
+      s0 += part[((long long)k * 2 + 0) * C + c];
+      q0 += part[((long long)k * 2 + 1) * C + c];
+      s1 += part[((long long)(k + G) * 2 + 0) * C + c];
+      q1 += part[((long long)(k + G) * 2 + 1) * C + c];
+    }
+    if (k < nchunk) {
+      s0 += part[((long long)k * 2 + 0) * C + c];
+      q0 += part[((long long)k * 2 + 1) * C + c];
     }
   }
-  sh[0][r][cl] = s;
-  sh[1][r][cl] = q;
+  sh[0][r][cl] = (double)s0 + (double)s1;
+  sh[1][r][cl] = (double)q0 + (double)q1;
   __syncthreads();
+  double s = 0.0, q = 0.0;
+  if (r == 0) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) { s += sh[0][j][cl]; q += sh[1][j][cl]; }
+  }
   if (r != 0 || c >= C) return;
-  s = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  q = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   const double invM = 1.0 / (double)M;
   const float g = gamma ? gamma[c] : 1.f;
   if (mode == 0) {
@@ -281,7 +293,7 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
   float* coef = ws + (long long)g.nchunk * 2 * C;
   dim3 grid(g.nchunk, g.gy);
   DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
-  bn_finalize_kernel<<<(C + 63) / 64, kBlk, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
                                                     momentum, eps, coef, nullptr, nullptr);
   DTG_TPR_SWITCH(g.tpr, {
     if (res) {
@@ -334,7 +346,7 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
     if (relu) bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
     else bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
   });
-  bn_finalize_kernel<<<(C + 63) / 64, kBlk, 0, st>>>(part, g.nchunk, M, C, 1, gamma, nullptr, nullptr, nullptr,
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 1, gamma, nullptr, nullptr, nullptr,
                                                     const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
                                                     coef, dgamma, dbeta);
   DTG_TPR_SWITCH(g.tpr, {

@@ -2,9 +2,10 @@
 //   C = act( alpha * op(A) * op(B) + beta * C + bias )
 // A is [M,K] (a_kc=1, lda = row stride) or stored K-major [K,M] (a_kc=0);
 // B is [N,K] (b_kc=1: nn.Linear weight layout) or [K,N] (b_kc=0).
-// Output fp32 or bf16.  split_k > 1 writes fp32 partial slabs to a workspace and a second pass
-// reduces them and applies the epilogue (deterministic; no atomics) -- used for weight-gradient
-// GEMMs whose K (= batch*H*W) is huge and whose output is a few tiles.
+// Output fp32 or bf16, written through an LDS-staged epilogue as 16-byte vectors.
+// split_k > 1 writes fp32 partial slabs to a workspace and a second pass reduces them and applies
+// the epilogue (deterministic; no atomics) -- used for weight-gradient GEMMs whose K
+// (= batch*H*W) is huge and whose output is a handful of tiles.
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
@@ -31,25 +32,46 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
-__device__ __forceinline__ void epi_store(const Epi& e, int M, int N, int m, int n, float v) {
-  if (m >= M || n >= N) return;
-  v *= e.alpha;
+// finish 8 consecutive columns [n, n+8) of row m (n < N; the tail is masked element-wise)
+__device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, float (&v)[8]) {
   const long long off = (long long)m * e.ldc + n;
-  if (e.beta != 0.f) v += e.beta * (e.c_bf16 ? bf2f(((const bf16_t*)e.C)[off]) : ((const float*)e.C)[off]);
-  if (e.bias) v += e.bias[n];
-  v = apply_act(v, e.act);
-  if (e.c_bf16) ((bf16_t*)e.C)[off] = f2bf(v);
-  else ((float*)e.C)[off] = v;
+  const int cnt = N - n < 8 ? N - n : 8;
+  const bool vec = cnt == 8 && ((e.ldc & 7) == 0);
+  float old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (e.beta != 0.f) {
+    if (vec) {
+      if (e.c_bf16) load8_bf16((const bf16_t*)e.C + off, old);
+      else load8_f32((const float*)e.C + off, old);
+    } else {
+      for (int k = 0; k < cnt; ++k)
+        old[k] = e.c_bf16 ? bf2f(((const bf16_t*)e.C)[off + k]) : ((const float*)e.C)[off + k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float x = v[k] * e.alpha + e.beta * old[k];
+    if (e.bias && k < cnt) x += e.bias[n + k];
+    v[k] = apply_act(x, e.act);
+  }
+  if (vec) {
+    if (e.c_bf16) store8_bf16((bf16_t*)e.C + off, v);
+    else store8_f32((float*)e.C + off, v);
+  } else {
+    for (int k = 0; k < cnt; ++k) {
+      if (e.c_bf16) ((bf16_t*)e.C)[off + k] = f2bf(v[k]);
+      else ((float*)e.C)[off + k] = v[k];
+    }
+  }
 }
 
-template <bool AKC, bool BKC, class SA, class SB>
+template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  const int ntiles = gridDim.x;  // (tiles_m * tiles_n) per split
+  __shared__ __attribute__((aligned(16))) char smem[CF::LDS_BYTES];
+  const int ntiles = gridDim.x;  // tiles per split
   const int t = xcd_remap(blockIdx.x, ntiles);
   const int tm = t / tiles_n, tn = t % tiles_n;
-  const int bm0 = tm * BM, bn0 = tn * BN;
+  const int bm0 = tm * CF::BM, bn0 = tn * CF::BN;
   const int split = blockIdx.y;
   const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
@@ -58,43 +80,44 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mainloop<AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
   if (split_k > 1) {
     float* slab = ws + (long long)split * M * N;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = bm0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-          const int n = bn0 + wn * 64 + j * 16 + (lane & 15);
-          if (m < M && n < N) slab[(long long)m * N + n] = acc[i][j][r];
-        }
+    const bool vec = (N & 3) == 0;
+    epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
+      float* p = slab + (long long)m * N + n;
+      if (vec && n + 8 <= N) store8_f32(p, v);
+      else
+        for (int k = 0; k < 8 && n + k < N; ++k) p[k] = v[k];
+    });
     return;
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        const int n = bn0 + wn * 64 + j * 16 + (lane & 15);
-        epi_store(e, M, N, m, n, acc[i][j][r]);
-      }
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
 }
 
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int split_k, int M, int N,
                                                             Epi e) {
-  const long long total = (long long)M * N;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < split_k; ++k) s += ws[(long long)k * total + i];
-    epi_store(e, M, N, (int)(i / N), (int)(i % N), s);
+  // 8 consecutive columns per thread
+  const int cgs = (N + 7) / 8;
+  const long long total = (long long)M * cgs;
+  const long long plane = (long long)M * N;
+  const bool vec = (N & 7) == 0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int m = (int)(i / cgs), n = (int)(i % cgs) * 8;
+    const long long off = (long long)m * N + n;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < split_k; ++k) {
+      if (vec) {
+        float v[8];
+        load8_f32(ws + k * plane + off, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[j];
+      } else {
+        for (int j = 0; j < 8 && n + j < N; ++j) s[j] += ws[k * plane + off + j];
+      }
+    }
+    epi_store8(e, N, m, n, s);
   }
 }
 
@@ -102,44 +125,55 @@ long long gemm_workspace_floats(int M, int N, int K, int split_k) {
   return split_k > 1 ? (long long)split_k * M * N : 0;
 }
 
+static bool skinny(int N) { return N <= 64; }
+
 int gemm_pick_split(int M, int N, int K) {
-  const long long tiles = (long long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int BMv = skinny(N) ? 256 : 128, BNv = skinny(N) ? 64 : 128;
+  const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   int s = 1;
-  // aim for >= ~512 workgroups (2 per CU over 256 CUs) while keeping >= 512 K per split
-  while (tiles * s < 512 && (long long)K / (s * 2) >= 512 && s < 64) s *= 2;
+  // aim for >= ~1024 workgroups (4 per CU) while keeping >= 1024 K (16 K-steps) per split
+  while (tiles * s < 1024 && (long long)K / (s * 2) >= 1024 && s < 512) s *= 2;
   return s;
+}
+
+template <class CF, bool AK, bool BK_>
+static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
+                   int kps, const Epi& e, float* ws, hipStream_t st) {
+  using SA = std::conditional_t<AK, DenseKC, DenseMC>;
+  using SB = std::conditional_t<BK_, DenseKC, DenseMC>;
+  SA sa{A, lda, M, K};
+  SB sb{B, ldb, N, K};
+  const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
+  dim3 grid(tiles_m * tiles_n, split_k);
+  hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(NT), 0, st, sa, sb, M, N, K, tiles_n, split_k,
+                     kps, e, ws);
+}
+
+template <class CF>
+static void launch_layout(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
+                          int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st) {
+  if (a_kc && b_kc) launch<CF, true, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else if (a_kc) launch<CF, true, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else if (b_kc) launch<CF, false, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else launch<CF, false, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
 }
 
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   if (split_k < 1) split_k = 1;
   int kps = (K + split_k - 1) / split_k;
   kps = (kps + BK - 1) / BK * BK;
+  if (kps < BK) kps = BK;
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act};
-  dim3 grid(tiles_m * tiles_n, split_k);
-  const size_t lds = 0;
-#define DTG_GEMM_LAUNCH(AK, BK_)                                                                              \
-  do {                                                                                                        \
-    using SA = std::conditional_t<AK, DenseKC, DenseMC>;                                                      \
-    using SB = std::conditional_t<BK_, DenseKC, DenseMC>;                                                     \
-    SA sa{A, lda, M, K};                                                                                      \
-    SB sb{B, ldb, N, K};                                                                                      \
-    hipLaunchKernelGGL((gemm_kernel<AK, BK_, SA, SB>), grid, dim3(NT), lds, st, sa, sb, M, N, K, tiles_n,    \
-                       split_k, kps, e, ws);                                                                  \
-  } while (0)
-  if (a_kc && b_kc) DTG_GEMM_LAUNCH(true, true);
-  else if (a_kc && !b_kc) DTG_GEMM_LAUNCH(true, false);
-  else if (!a_kc && b_kc) DTG_GEMM_LAUNCH(false, true);
-  else DTG_GEMM_LAUNCH(false, false);
-#undef DTG_GEMM_LAUNCH
+  if (skinny(N)) launch_layout<Cfg<256, 64>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else launch_layout<Cfg<128, 128>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
   if (split_k > 1) {
-    const long long total = (long long)M * N;
-    splitk_reduce_kernel<<<grid_for(total, 256, 2048), 256, 0, st>>>(ws, split_k, M, N, e);
+    const long long total = (long long)M * ((N + 7) / 8);
+    splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
   }
 }
 

@@ -11,7 +11,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from ._native import lib
+from ..parallel import grad_sink
 from .gemm import gemm
 
 _IMPL = os.environ.get("DTG_CONV_IMPL", "dtg")
@@ -36,6 +36,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.save_for_backward(x2, w2)
         ctx.shape = (n, c, h, wd)
         ctx.wshape = w.shape
+        ctx.param = w if grad_sink.enabled(w) else None
         return y2.view(n, h, wd, cout).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -43,9 +44,15 @@ class _Conv1x1(torch.autograd.Function):
         x2, w2 = ctx.saved_tensors
         n, c, h, wd = ctx.shape
         dy2 = _rows(dy)
-        dx2 = gemm(dy2, True, w2, False)
+        dx2 = gemm(dy2, True, w2, False) if ctx.needs_input_grad[0] else None
+        dx = dx2.view(n, h, wd, c).permute(0, 3, 1, 2) if dx2 is not None else None
+        p = ctx.param
+        if p is not None:
+            # wgrad accumulates straight into the flat gradient buffer (beta = 1)
+            gemm(dy2, False, x2, False, out=p.grad.view(w2.shape), beta=1.0)
+            grad_sink.notify(p)
+            return dx, None
         dw2 = gemm(dy2, False, x2, False)
-        dx = dx2.view(n, h, wd, c).permute(0, 3, 1, 2)
         return dx, dw2.view(ctx.wshape)
 
 

@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from ._native import lib
+from ..parallel import grad_sink
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
 
@@ -47,6 +48,7 @@ class _Linear(torch.autograd.Function):
         ctx.act = act
         ctx.has_bias = b is not None
         ctx.bias_dtype = b.dtype if b is not None else None
+        ctx.param = w if grad_sink.enabled(w) else None
         ctx.save_for_backward(x2, w, pre if act == "gelu" else (y if act == "relu" else None))
         return y
 
@@ -58,9 +60,14 @@ class _Linear(torch.autograd.Function):
             dy = gelu_bwd(dy, saved)
         elif ctx.act == "relu":
             dy = dy * (saved > 0)
-        dx = gemm(dy, True, w, False)                      # [M,K]
-        dw = gemm(dy, False, x2, False, out_dtype=w.dtype)  # [N,K]
+        dx = gemm(dy, True, w, False) if ctx.needs_input_grad[0] else None  # [M,K]
         db = dy.float().sum(0).to(ctx.bias_dtype) if ctx.has_bias else None
+        p = ctx.param
+        if p is not None:
+            gemm(dy, False, x2, False, out=p.grad, beta=1.0)  # wgrad straight into the flat buffer
+            grad_sink.notify(p)
+            return dx, None, db, None
+        dw = gemm(dy, False, x2, False, out_dtype=w.dtype)  # [N,K]
         return dx, dw, db, None
 
 

@@ -20,6 +20,8 @@ Design:
 import torch
 import torch.distributed as dist
 
+from . import grad_sink
+
 
 class _Bucket:
     __slots__ = ("group", "start", "end", "params", "pending", "work", "index")
@@ -63,6 +65,7 @@ class DataParallel:
         if self.overlap:
             for p in self._param_bucket:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            grad_sink.add_listener(self._on_direct)
         self._reset()
 
     # -- hooks ---------------------------------------------------------------------------------
@@ -73,6 +76,10 @@ class DataParallel:
 
     def _launch(self, b):
         b.work = dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def _on_direct(self, p):
+        if p in self._param_bucket:
+            self._on_grad(p)
 
     def _on_grad(self, p):
         b = self._param_bucket[p]
@@ -113,3 +120,4 @@ class DataParallel:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        grad_sink.remove_listener(self._on_direct)

@@ -20,6 +20,8 @@ from collections import OrderedDict
 
 import torch
 
+from . import grad_sink
+
 ALIGN = 64  # elements; keeps every view 128-byte aligned for 16-B vector access
 
 
@@ -63,6 +65,7 @@ class FlatGroup:
                     v.copy_(p.detach().to(compute_dtype))
                 p.data = v
                 p.grad = _view_like(self.grad, o, p)
+                grad_sink.mark(p)
 
     def state_buffer(self, key):
         """Lazily allocated fp32 optimizer state with the master's layout."""

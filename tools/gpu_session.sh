@@ -28,6 +28,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
+    kbench) run kbench 600 python tools/bench_kernels.py --json gpurun_out/kbench.json ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
             python3 bench.py --steps 5 --warmup 3 ;;
     *) run "$s" 900 bash -c "$s" ;;
