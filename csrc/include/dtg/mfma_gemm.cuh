@@ -7,7 +7,12 @@
 //   Cfg<128,128>  2x2 waves  -- general
 //   Cfg<256, 64>  4x1 waves  -- skinny N (64-channel convs): A streamed once, no wasted MFMAs
 // Operand tiles are staged HBM->LDS with global_load_lds_dwordx4 (LDS-DMA, 1 KiB per
-// wave-instruction, no VGPR round trip) into a 2-deep LDS ring, one barrier per K-step.
+// wave-instruction, no VGPR round trip).  STAGES = 2: 2-deep LDS ring, next tile's DMA in flight
+// under the current tile's MFMAs, one barrier per K-step; STAGES = 1 (short K): half the LDS, so
+// twice the workgroups per CU hide latency across blocks instead.
+//
+// All LDS accesses go through address_space(3) pointers: a generic pointer makes hipcc emit
+// flat_load (counted on vmcnt AND lgkmcnt), which drains the in-flight DMA at every fragment read.
 //
 // Each operand is either
 //   KC  ("K-contiguous")  : element (row, k) at base(row) + k          -> LDS [rows][64]  128 B rows,
@@ -20,7 +25,8 @@
 //
 // Where an operand comes from is a policy object (`Src`) returning the global address of the
 // 16-byte chunk a lane must fetch; dense strided matrices and im2col gathers (conv.hip) plug in
-// here.  A chunk that lies outside the matrix returns the address of a zero page.
+// here.  GUARD=false instantiations (every tile full) compute addresses with no bounds checks;
+// GUARD=true ones send out-of-range chunks to a zero page.
 #pragma once
 #include "dtg/common.h"
 
@@ -30,27 +36,36 @@ namespace gemm {
 typedef __attribute__((ext_vector_type(8))) __bf16 v8bf;
 typedef __attribute__((ext_vector_type(4))) __bf16 v4bf;
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) v4bf lds_v4bf;
+typedef __attribute__((address_space(3))) v8bf lds_v8bf;
+typedef __attribute__((address_space(3))) float lds_float;
 
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-template <int BM_, int BN_>
+template <int BM_, int BN_, int STAGES_ = 2>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_;
   static constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == 4, "4 waves of 64x64");
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
-  // epilogue staging: 64 rows x (BN+4) fp32 must fit in the (then idle) operand ring
-  static_assert(64 * (BN + 4) * 4 <= LDS_BYTES, "epilogue staging does not fit");
+  static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
+  static constexpr int EPI_ROWS = 32;  // epilogue staging pass height
+  static_assert(EPI_ROWS * (BN + 4) * 4 <= LDS_BYTES, "epilogue staging does not fit");
 };
 
 // 16-byte zero page in global memory for out-of-range chunks (glds needs a global source).
 __device__ __attribute__((aligned(64))) static const bf16_t g_zero_page[32] = {0};
 
 __device__ __forceinline__ const void* zero_src() { return (const void*)g_zero_page; }
+
+// branch-free select between a real chunk address and the zero page
+__device__ __forceinline__ const void* sel(bool ok, const void* p) {
+  const uintptr_t a = (uintptr_t)p, z = (uintptr_t)zero_src();
+  return (const void*)(ok ? a : z);
+}
 
 // swizzle of the 16-B chunk index of an MC row (CH chunks): keeps 32-B pairs together and makes
 // the 8 rows read by one ds_read_b64_tr_b16 half-wave distinct where the row is wide enough
@@ -61,31 +76,36 @@ __device__ __forceinline__ int mc_swz(int k) {
 
 // ---- dense sources -------------------------------------------------------------------------
 // KC: matrix stored [rows][ld] with k contiguous
+template <bool GUARD>
 struct DenseKC {
   const bf16_t* p;
   long long ld;
   int rows, K;
   __device__ __forceinline__ const void* chunk(int row, int k) const {
-    if (k >= K) return zero_src();
-    if (row >= rows) row = rows - 1;
-    return p + (long long)row * ld + k;
+    if constexpr (!GUARD) return p + (long long)row * ld + k;
+    const int r = row < rows ? row : rows - 1;
+    return sel(k < K, p + (long long)r * ld + k);
   }
 };
 // MC: matrix stored [K][ld] with the row/col (M or N) index contiguous
+template <bool GUARD>
 struct DenseMC {
   const bf16_t* p;
   long long ld;
   int cols, K;
   __device__ __forceinline__ const void* chunk(int krow, int col) const {
-    if (krow >= K || col >= cols) return zero_src();
-    return p + (long long)krow * ld + col;
+    if constexpr (!GUARD) return p + (long long)krow * ld + col;
+    const bool ok = krow < K && col < cols;
+    const int kr = krow < K ? krow : K - 1;
+    const int cc = col < cols ? col : 0;
+    return sel(ok, p + (long long)kr * ld + cc);
   }
 };
 
 // ---- staging ---------------------------------------------------------------------------------
 // KC tile: ROWS x 64 k (128 B rows); a wave-instruction covers 8 rows
 template <int ROWS, class Src>
-__device__ __forceinline__ void stage_kc(const Src& src, char* lds_tile, int row0, int k0, int wave, int lane) {
+__device__ __forceinline__ void stage_kc(const Src& src, lds_char* lds_tile, int row0, int k0, int wave, int lane) {
   constexpr int PER_WAVE = ROWS / 32;
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
@@ -100,7 +120,7 @@ __device__ __forceinline__ void stage_kc(const Src& src, char* lds_tile, int row
 
 // MC tile: 64 k-rows x ROWS cols (2*ROWS B rows); a wave-instruction covers 512/ROWS k-rows
 template <int ROWS, class Src>
-__device__ __forceinline__ void stage_mc(const Src& src, char* lds_tile, int col0, int k0, int wave, int lane) {
+__device__ __forceinline__ void stage_mc(const Src& src, lds_char* lds_tile, int col0, int k0, int wave, int lane) {
   constexpr int CH = ROWS / 8;          // 16-B chunks per k-row
   constexpr int KPI = 64 / CH;          // k-rows per wave-instruction
   constexpr int PER_WAVE = 64 / KPI / 4;
@@ -117,113 +137,134 @@ __device__ __forceinline__ void stage_mc(const Src& src, char* lds_tile, int col
 
 // ---- fragment reads (one 16x32 operand fragment for mfma_f32_16x16x32_bf16) --------------------
 // lane l holds X[r0 + (l&15)][ks*32 + 8*(l>>4) + j], j = 0..7
-__device__ __forceinline__ v8bf frag_kc(const char* lds_tile, int r0, int ks, int lane) {
+__device__ __forceinline__ v8bf frag_kc(const lds_char* lds_tile, int r0, int ks, int lane) {
   const int r = r0 + (lane & 15);
   const int c = ks * 4 + (lane >> 4);
-  return *reinterpret_cast<const v8bf*>(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
+  return *reinterpret_cast<const lds_v8bf*>(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
 }
 
 template <int ROWS>
-__device__ __forceinline__ v8bf frag_mc(const char* lds_tile, int r0, int ks, int lane) {
+__device__ __forceinline__ v8bf frag_mc(const lds_char* lds_tile, int r0, int ks, int lane) {
   constexpr int CH = ROWS / 8;
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int kA = ks * 32 + 8 * g + q;   // rows for elements 0..3
   const int kB = kA + 4;                // rows for elements 4..7
   const int ch = (r0 >> 3) + (p >> 1);  // 16-B chunk of columns r0+4p .. r0+4p+3
   const int sub = (p & 1) * 8;
-  const char* a = lds_tile + kA * ROWS * 2 + ((ch ^ mc_swz<CH>(kA)) << 4) + sub;
-  const char* b = lds_tile + kB * ROWS * 2 + ((ch ^ mc_swz<CH>(kB)) << 4) + sub;
+  const lds_char* a = lds_tile + kA * ROWS * 2 + ((ch ^ mc_swz<CH>(kA)) << 4) + sub;
+  const lds_char* b = lds_tile + kB * ROWS * 2 + ((ch ^ mc_swz<CH>(kB)) << 4) + sub;
   const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(a));
   const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(b));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 template <bool KC, int ROWS>
-__device__ __forceinline__ v8bf frag(const char* t, int r0, int ks, int lane) {
+__device__ __forceinline__ v8bf frag(const lds_char* t, int r0, int ks, int lane) {
   if constexpr (KC) return frag_kc(t, r0, ks, lane);
   else return frag_mc<ROWS>(t, r0, ks, lane);
 }
 
 template <bool KC, int ROWS, class Src>
-__device__ __forceinline__ void stage(const Src& s, char* t, int rc0, int k0, int wave, int lane) {
+__device__ __forceinline__ void stage(const Src& s, lds_char* t, int rc0, int k0, int wave, int lane) {
   if constexpr (KC) stage_kc<ROWS>(s, t, rc0, k0, wave, lane);
   else stage_mc<ROWS>(s, t, rc0, k0, wave, lane);
+}
+
+template <class C, bool AKC, bool BKC>
+__device__ __forceinline__ void compute_tile(const lds_char* At, const lds_char* Bt, int wm, int wn, int lane,
+                                             f32x4 (&acc)[4][4]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    v8bf a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = frag<AKC, C::BM>(At, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = frag<BKC, C::BN>(Bt, wn * 64 + j * 16, ks, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
 }
 
 // ---- main loop -------------------------------------------------------------------------------
 // Accumulates the K range [kbeg, kend) of tile (bm0, bn0) into acc[4][4].
 template <class C, bool AKC, bool BKC, class SA, class SB>
-__device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, char* smem, int bm0, int bn0, int kbeg, int kend,
-                                         f32x4 (&acc)[4][4]) {
+__device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* smem, int bm0, int bn0, int kbeg,
+                                         int kend, f32x4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
-  char* As[2] = {smem, smem + C::STAGE_BYTES};
-  char* Bs[2] = {smem + C::A_BYTES, smem + C::STAGE_BYTES + C::A_BYTES};
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk <= 0) return;
-  stage<AKC, C::BM>(sa, As[0], bm0, kbeg, wave, lane);
-  stage<BKC, C::BN>(sb, Bs[0], bn0, kbeg, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      stage<AKC, C::BM>(sa, As[cur ^ 1], bm0, kbeg + (kt + 1) * BK, wave, lane);
-      stage<BKC, C::BN>(sb, Bs[cur ^ 1], bn0, kbeg + (kt + 1) * BK, wave, lane);
+  if constexpr (C::STAGES == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      stage<AKC, C::BM>(sa, smem, bm0, kbeg + kt * BK, wave, lane);
+      stage<BKC, C::BN>(sb, smem + C::A_BYTES, bn0, kbeg + kt * BK, wave, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute_tile<C, AKC, BKC>(smem, smem + C::A_BYTES, wm, wn, lane, acc);
+      __syncthreads();
     }
-    const char* At = As[cur];
-    const char* Bt = Bs[cur];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      v8bf a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag<AKC, C::BM>(At, wm * 64 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = frag<BKC, C::BN>(Bt, wn * 64 + j * 16, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+  } else {
+    stage<AKC, C::BM>(sa, smem, bm0, kbeg, wave, lane);
+    stage<BKC, C::BN>(sb, smem + C::A_BYTES, bn0, kbeg, wave, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = (kt & 1) * C::STAGE_BYTES, nxt = C::STAGE_BYTES - cur;
+      if (kt + 1 < nk) {
+        stage<AKC, C::BM>(sa, smem + nxt, bm0, kbeg + (kt + 1) * BK, wave, lane);
+        stage<BKC, C::BN>(sb, smem + nxt + C::A_BYTES, bn0, kbeg + (kt + 1) * BK, wave, lane);
+      }
+      compute_tile<C, AKC, BKC>(smem + cur, smem + cur + C::A_BYTES, wm, wn, lane, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 }
 
 // ---- epilogue ----------------------------------------------------------------------------------
-// Stages the block's fp32 accumulators through LDS (64 rows at a time) so that every global
-// store is a coalesced 16-byte vector; OP(row, col0, float (&v)[8]) finishes 8 consecutive
+// Stages the block's fp32 accumulators through LDS (EPI_ROWS rows at a time) so that every
+// global store is a coalesced 16-byte vector; OP(row, col0, float (&v)[8]) finishes 8 consecutive
 // columns (bias, residual/beta, activation, dtype) and stores them.
 template <class C, class OP>
-__device__ __forceinline__ void epilogue_staged(char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+__device__ __forceinline__ void epilogue_staged(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                                 const OP& op) {
   constexpr int LD = C::BN + 4;  // fp32 row pitch (pad breaks bank aliasing of the column writes)
-  float* st = reinterpret_cast<float*>(smem);
+  constexpr int R = C::EPI_ROWS;
+  lds_float* st = reinterpret_cast<lds_float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WN, wn = wave % C::WN;
   __syncthreads();  // operand ring no longer read by anyone
 #pragma unroll
-  for (int pass = 0; pass < C::WM; ++pass) {
-    if (wm == pass) {
+  for (int pass = 0; pass < C::BM / R; ++pass) {
+    // rows [pass*R, pass*R + R) belong to wave-row wm = pass*R/64, i-blocks (pass*R%64)/16 ...
+    const int prow0 = pass * R;
+    if (wm == prow0 / 64) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int rblk = (i * 16) - (prow0 % 64);  // row offset of this i-block inside the pass
+        if (rblk >= 0 && rblk < R) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            st[(i * 16 + (lane >> 4) * 4 + r) * LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+              st[(rblk + (lane >> 4) * 4 + r) * LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+      }
     }
     __syncthreads();
     constexpr int CPR = C::BN / 8;  // 8-column groups per row
-    for (int idx = tid; idx < 64 * CPR; idx += NT) {
+#pragma unroll
+    for (int idx = tid; idx < R * CPR; idx += NT) {
       const int rr = idx / CPR, cg = idx % CPR;
-      const int m = bm0 + pass * 64 + rr, n = bn0 + cg * 8;
+      const int m = bm0 + prow0 + rr, n = bn0 + cg * 8;
       if (m < M && n < N) {
         float v[8];
-        const float4 a = *reinterpret_cast<const float4*>(st + rr * LD + cg * 8);
-        const float4 b = *reinterpret_cast<const float4*>(st + rr * LD + cg * 8 + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        const lds_float* s = st + rr * LD + cg * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = s[k];
         op(m, n, v);
       }
     }

@@ -67,7 +67,8 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
 template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) char smem[CF::LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
   const int ntiles = gridDim.x;  // tiles per split
   const int t = xcd_remap(blockIdx.x, ntiles);
   const int tm = t / tiles_n, tn = t % tiles_n;
@@ -121,6 +122,36 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Parallel split-K reduction: a block owns 256 consecutive outputs (32 lanes x 8 floats) and its
+// 8 lane-groups stride over the splits; partial sums meet in LDS.  Needs (M*N) % 8 == 0, N % 8 == 0.
+__global__ void __launch_bounds__(256) splitk_reduce_par_kernel(const float* __restrict__ ws, int split_k, int M,
+                                                                int N, Epi e) {
+  __shared__ float red[8][256 + 8];
+  const long long plane = (long long)M * N;
+  const long long base = (long long)blockIdx.x * 256;
+  const int lane = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (base + lane * 8 < plane) {
+    for (int k = grp; k < split_k; k += 8) {
+      float v[8];
+      load8_f32(ws + k * plane + base + lane * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[grp][lane * 8 + j] = s[j];
+  __syncthreads();
+  if (grp == 0 && base + lane * 8 < plane) {
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += red[g][lane * 8 + j];
+    const long long i = base + lane * 8;
+    epi_store8(e, N, (int)(i / N), (int)(i % N), s);
+  }
+}
+
 long long gemm_workspace_floats(int M, int N, int K, int split_k) {
   return split_k > 1 ? (long long)split_k * M * N : 0;
 }
@@ -131,16 +162,17 @@ int gemm_pick_split(int M, int N, int K) {
   const int BMv = skinny(N) ? 256 : 128, BNv = skinny(N) ? 64 : 128;
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   int s = 1;
-  // aim for >= ~1024 workgroups (4 per CU) while keeping >= 1024 K (16 K-steps) per split
-  while (tiles * s < 1024 && (long long)K / (s * 2) >= 1024 && s < 512) s *= 2;
+  // aim for >= ~512 workgroups (2 per CU: the LDS ring admits 2) while keeping >= 1024 K
+  // (16 K-steps) per split
+  while (tiles * s < 512 && (long long)K / (s * 2) >= 1024 && s < 256) s *= 2;
   return s;
 }
 
-template <class CF, bool AK, bool BK_>
+template <class CF, bool AK, bool BK_, bool GUARD>
 static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
                    int kps, const Epi& e, float* ws, hipStream_t st) {
-  using SA = std::conditional_t<AK, DenseKC, DenseMC>;
-  using SB = std::conditional_t<BK_, DenseKC, DenseMC>;
+  using SA = std::conditional_t<AK, DenseKC<GUARD>, DenseMC<GUARD>>;
+  using SB = std::conditional_t<BK_, DenseKC<GUARD>, DenseMC<GUARD>>;
   SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
@@ -149,13 +181,29 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
                      kps, e, ws);
 }
 
-template <class CF>
+template <class CF, bool GUARD>
 static void launch_layout(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
                           int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st) {
-  if (a_kc && b_kc) launch<CF, true, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else if (a_kc) launch<CF, true, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else if (b_kc) launch<CF, false, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else launch<CF, false, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  if (a_kc && b_kc) launch<CF, true, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else if (a_kc) launch<CF, true, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else if (b_kc) launch<CF, false, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else launch<CF, false, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+}
+
+template <int BM_, int BN_>
+static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
+                       int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st) {
+  // full tiles -> no bounds checks in the address computation
+  const bool full = (M % BM_ == 0) && (N % BN_ == 0) && (K % BK == 0);
+  // short K per block -> single-stage ring (half the LDS, 2x the resident workgroups)
+  const bool short_k = kps <= 2 * BK;
+  if (full) {
+    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+    else launch_layout<Cfg<BM_, BN_, 2>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  } else {
+    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+    else launch_layout<Cfg<BM_, BN_, 2>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  }
 }
 
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
@@ -169,11 +217,16 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act};
-  if (skinny(N)) launch_layout<Cfg<256, 64>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else launch_layout<Cfg<128, 128>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
   if (split_k > 1) {
-    const long long total = (long long)M * ((N + 7) / 8);
-    splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
+    if (N % 8 == 0) {
+      const long long plane = (long long)M * N;
+      splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e);
+    } else {
+      const long long total = (long long)M * ((N + 7) / 8);
+      splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
+    }
   }
 }
 
