@@ -96,8 +96,8 @@ class Server:
         self._started = False
         if start:
             self.start()
-        from . import framework
-        framework._register_server(self)
+        from . import graph
+        graph._register_server(self)
 
     def start(self):
         if not self._started:

@@ -1,0 +1,224 @@
+"""SyncReplicasOptimizer (SURVEY §2.3 "Synchronous SGD", §2.5 N6/N7, §7.5 item 4).
+
+Two execution modes behind one API:
+
+* **PS-accumulator mode** (the reference's semantics; used whenever the variables live on a PS or
+  ``replicas_to_aggregate < total_num_replicas``): every worker pushes its gradients into a
+  per-variable ConditionalAccumulator on the PS (stale gradients, whose ``local_step`` is behind the
+  accumulator's global step, are dropped), then blocks on the sync-token queue.  The chief runs an
+  aggregation thread (TF's chief QueueRunner): take ``replicas_to_aggregate`` gradients per
+  variable (their mean), apply them with the wrapped optimizer on the PS, bump ``global_step``,
+  advance the accumulators and enqueue one token per replica.  With M workers aggregating N < M,
+  M - N gradients per step are backups and get dropped (Synchronous-SGD/README.md:3).
+  Native pieces: csrc/ps/server.cc ACC_* and Q_* ops.
+
+* **All-reduce mode** (``dtg.parallel.DataParallel``): no PS, one gradient per rank, bucketed RCCL
+  all-reduce overlapped with backward -- the fast path for the north-star models.  See
+  ``SyncReplicasOptimizer.allreduce()``.
+"""
+import threading
+import time
+
+import numpy as np
+import torch
+
+from .. import graph as G
+from ..graph import Op, Tensor
+from ..variables import Variable, _as_np
+from .hooks import SessionRunHook
+from .optimizer import Optimizer
+
+TOKEN_QUEUE = "sync_token_q"
+
+
+class SyncReplicasOptimizer(Optimizer):
+    def __init__(self, opt, replicas_to_aggregate, total_num_replicas=None, variable_averages=None,
+                 variables_to_average=None, use_locking=False, name="sync_replicas"):
+        super().__init__(opt._lr, use_locking, name)
+        self._opt = opt
+        self._replicas_to_aggregate = int(replicas_to_aggregate)
+        self._total_num_replicas = int(total_num_replicas or replicas_to_aggregate)
+        self._tokens_per_step = max(self._total_num_replicas, self._replicas_to_aggregate)
+        self._gv = None
+        self._global_step = None
+        self.local_step = 0
+        self._stop_check = None
+        self._chief_thread = None
+        self._chief_stop = threading.Event()
+        self.dropped = 0
+        # strict lock-step (dtg extension, enabled by num_tokens == 0 in the hook): one token queue
+        # per worker, so every replica contributes exactly one fresh gradient per global step
+        self.strict = False
+
+    def _token_queue(self, task=None):
+        if not self.strict:
+            return TOKEN_QUEUE
+        if task is None:
+            from ..variables import _this_server
+            s = _this_server()
+            task = s.task_index if s is not None else 0
+        return "%s/%d" % (TOKEN_QUEUE, task)
+
+    # ------------------------------------------------------------------------------------------
+    def compute_gradients(self, *args, **kwargs):
+        return self._opt.compute_gradients(*args, **kwargs)
+
+    def apply_gradients(self, grads_and_vars, global_step=None, name=None):
+        if global_step is None:
+            raise ValueError("SyncReplicasOptimizer.apply_gradients needs global_step")
+        self._gv = [(g, v) for g, v in grads_and_vars]
+        self._global_step = global_step
+        for _, v in self._gv:
+            if not (isinstance(v, Variable) and v.remote):
+                raise ValueError("PS-accumulator mode needs variables on a parameter server; for PS-less "
+                                 "synchronous training use dtg.parallel.DataParallel (all-reduce mode)")
+        self.chief_init_op = Op(lambda c: self._init_local_step(), [], "sync_rep_local_step_init")
+        self.local_step_init_op = self.chief_init_op
+        self.ready_for_local_init_op = _ReadyForLocalInit(self)
+        return _SyncTrainOp(self, name or "sync_replicas_train")
+
+    # ------------------------------------------------------------------------------------------
+    def _acc_name(self, v):
+        return v._name + "/grad_accum"
+
+    def _gs_client(self):
+        return self._global_step._client()
+
+    def _read_gs(self):
+        return int(self._global_step.read_value().item())
+
+    def _ensure_accumulators(self, step=None):
+        step = self._read_gs() if step is None else step
+        for _, v in self._gv:
+            v._client().acc_create(self._acc_name(v), np.zeros(v.shape, np.float32), int(step))
+
+    def _init_local_step(self):
+        self.local_step = self._read_gs()
+        self._ensure_accumulators(self.local_step)
+
+    def get_init_tokens_op(self, num_tokens=-1):
+        tokens_needed = self._replicas_to_aggregate - self._total_num_replicas
+        if num_tokens == -1:
+            num_tokens = self._replicas_to_aggregate
+        elif num_tokens < tokens_needed:
+            raise ValueError("Too few tokens to finish the first step: %d (given) vs %d (needed)"
+                             % (num_tokens, tokens_needed))
+
+        def run(ctx):
+            if num_tokens > 0:
+                gs = self._read_gs()
+                self._gs_client().q_enqueue(TOKEN_QUEUE, [gs] * num_tokens)
+        return Op(run, [], "sync_replicas/init_tokens")
+
+    def make_session_run_hook(self, is_chief, num_tokens=-1):
+        return _SyncReplicasHook(self, is_chief, num_tokens)
+
+    # ---- chief aggregation loop (TF: get_chief_queue_runner) ---------------------------------
+    def _chief_loop(self):
+        opt = self._opt
+        gv = self._gv
+        gs = self._global_step
+        while not self._chief_stop.is_set():
+            grads = []
+            for _, v in gv:
+                g = None
+                while g is None and not self._chief_stop.is_set():
+                    g = v._client().acc_take(self._acc_name(v), self._replicas_to_aggregate, 0.25)
+                if g is None:
+                    return
+                grads.append(g)
+            lr = float(opt._lr) if not isinstance(opt._lr, Tensor) else float(G.RunContext().eval(opt._lr))
+            opt._t += 1
+            by_task = {}
+            for g, (_, v) in zip(grads, gv):
+                by_task.setdefault(v.ps_task, []).append((v._name, np.array(g, dtype=np.float32, order="C")))
+            new_step = None
+            for task, items in by_task.items():
+                gs_name = gs._name if (gs.remote and gs.ps_task == task and new_step is None) else ""
+                client = [v for _, v in gv if v.ps_task == task][0]._client()
+                step, _ = client.apply(opt.PS_KIND, opt._hyper(lr), bool(opt._use_locking), gs_name, items, False)
+                if gs_name:
+                    new_step = step
+            if new_step is None:
+                new_step = int(gs._client().assign_add(gs._name, np.ones((), _np(gs.dtype))))
+            for _, v in gv:
+                v._client().acc_set_step(self._acc_name(v), int(new_step))
+            if self.strict:
+                for t in range(self._total_num_replicas):
+                    self._gs_client().q_enqueue(self._token_queue(t), [int(new_step)])
+            else:
+                self._gs_client().q_enqueue(TOKEN_QUEUE, [int(new_step)] * self._tokens_per_step)
+
+    def start_chief(self):
+        if self._chief_thread is None:
+            self._chief_stop.clear()
+            self._chief_thread = threading.Thread(target=self._chief_loop, name="sync_replicas_chief", daemon=True)
+            self._chief_thread.start()
+
+    def stop_chief(self):
+        self._chief_stop.set()
+        if self._chief_thread is not None:
+            self._chief_thread.join(timeout=5)
+            self._chief_thread = None
+
+
+def _np(dt):
+    return {torch.int32: np.int32, torch.int64: np.int64}.get(dt, np.float32)
+
+
+class _ReadyForLocalInit(Tensor):
+    def __init__(self, opt):
+        self._opt = opt
+        super().__init__(lambda c: None, [], "report_uninitialized_variables_1")
+
+    def _eval(self, ctx):
+        names = [v._name for _, v in self._opt._gv if not v.is_initialized()]
+        if not self._opt._global_step.is_initialized():
+            names.append(self._opt._global_step._name)
+        return np.array(names, dtype=object)
+
+
+class _SyncTrainOp(Op):
+    """Worker side of one synchronous step: push grads into the accumulators, wait for a token."""
+
+    def __init__(self, sro, name):
+        self.sro = sro
+        super().__init__(lambda c: None, [g for g, _ in sro._gv], name)
+
+    def _eval(self, ctx):
+        sro = self.sro
+        grads = [ctx.eval(g) for g, _ in sro._gv]
+        for g, (_, v) in zip(grads, sro._gv):
+            ok = v._client().acc_apply(sro._acc_name(v), int(sro.local_step), _as_np(g.float()))
+            if not ok:
+                sro.dropped += 1
+        client = sro._gs_client()
+        while True:
+            tok = client.q_dequeue(sro._token_queue(), 0.5)
+            if tok is not None:
+                sro.local_step = int(tok)
+                return None
+            sess = ctx.session
+            if sess is not None and sess._stop_requested_externally():
+                return None
+
+
+class _SyncReplicasHook(SessionRunHook):
+    def __init__(self, sro, is_chief, num_tokens):
+        self._sro = sro
+        self._is_chief = is_chief
+        self._num_tokens = num_tokens
+        sro.strict = num_tokens == 0
+
+    def after_create_session(self, session, coord):
+        sro = self._sro
+        if self._is_chief:
+            sro._init_local_step()
+            G.RunContext(session).eval(sro.get_init_tokens_op(self._num_tokens))
+            sro.start_chief()
+        else:
+            sro._init_local_step()
+
+    def end(self, session):
+        if self._is_chief:
+            self._sro.stop_chief()

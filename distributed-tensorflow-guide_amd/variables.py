@@ -75,7 +75,7 @@ def _as_np(t):
     t = t.detach()
     if t.dtype == torch.bfloat16:
         t = t.float()
-    return np.ascontiguousarray(t.cpu().numpy())
+    return np.array(t.cpu().numpy(), order="C", copy=True)  # keeps 0-d shapes (ascontiguousarray does not)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -137,7 +137,7 @@ class Variable(Tensor):
     def _initial_tensor(self, peek=False):
         v = self._init
         if isinstance(v, Node):
-            if peek:
+            if peek and (v.inputs or v.control_inputs or isinstance(v, Variable)):
                 return None
             v = G.RunContext().eval(v)
         if callable(v) and not isinstance(v, torch.Tensor):

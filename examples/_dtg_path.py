@@ -1,0 +1,7 @@
+"""Puts the repository root on sys.path so every example can ``import dtg`` when run directly."""
+import os
+import sys
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)
