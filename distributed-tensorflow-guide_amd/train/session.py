@@ -177,8 +177,10 @@ class _Session:
         return to_numpy(RunContext(self, feed_dict).eval(fetches))
 
     def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
-        if self._should_stop and self.hooks:
-            raise RuntimeError("Run called even after should_stop requested.")
+        # TF raises "Run called even after should_stop requested." here, which makes the reference's
+        # bootstrap runs crash when a finished job is resumed from its checkpoint (the first run's
+        # StopAtStepHook already requests the stop).  dtg keeps running the fetches; the training
+        # loop's should_stop() check then ends the job cleanly.
         rc = SessionRunContext(SessionRunArgs(fetches, feed_dict), self)
         hargs = [h.before_run(rc) for h in self.hooks]
         feed = dict(feed_dict or {})

@@ -1,0 +1,9 @@
+#!/bin/bash
+# ADAG: 1 PS + 2 asynchronous workers, averaged T=3 window.
+# Extra flags are forwarded, e.g. ./run.sh --observe_sleep 0 --cluster '{"ps":[...],"worker":[...]}'
+# The parameter server exits by itself once every worker has finished (no pkill needed).
+cd "$(dirname "$0")"
+python ADAG.py --job_name "ps" --task_index 0 "$@" &
+python ADAG.py --job_name "worker" --task_index 0 "$@" &
+python ADAG.py --job_name "worker" --task_index 1 "$@" &
+wait

@@ -1,0 +1,9 @@
+#!/bin/bash
+# SDAG (synchronous, windowed): 1 PS + 2 workers.
+# Extra flags are forwarded, e.g. ./run.sh --observe_sleep 0 --cluster '{"ps":[...],"worker":[...]}'
+# The parameter server exits by itself once every worker has finished (no pkill needed).
+cd "$(dirname "$0")"
+python dist_cpu_sing_mach_sync.py --job_name "ps" --task_index 0 "$@" &
+python dist_cpu_sing_mach_sync.py --job_name "worker" --task_index 0 "$@" &
+python dist_cpu_sing_mach_sync.py --job_name "worker" --task_index 1 "$@" &
+wait

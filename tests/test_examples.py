@@ -1,0 +1,160 @@
+"""Integration tests: every reference example run as a localhost multi-process cluster on the CPU,
+checked against the analytic oracles of SURVEY §4.3 (TF is not installed, so these closed-form
+end states replace running the reference) or, where interleaving makes values timing-dependent,
+against invariants (global_step reaches last_step, c moves monotonically toward 100, every task
+exits -- including the parameter server, which the reference has to pkill)."""
+import os
+
+import pytest
+
+from _cluster import last_int_after, last_vector, run_cluster
+
+
+def _ok(out):
+    for (job, t), (rc, o) in out.items():
+        assert rc == 0, "%s:%d exited %s\n%s" % (job, t, rc, o[-3000:])
+
+
+def test_downpour_one_worker_oracle(tmp_path):
+    out = run_cluster("DOWNPOUR/DOWNPOUR.py", 1, 1, ["--logdir", str(tmp_path / "logdir")])
+    _ok(out)
+    w = out[("worker", 0)][1]
+    assert abs(last_vector(w, "global step") - 0.00281919) < 1e-7
+    assert last_int_after(w, "global step:") == 60
+    assert last_int_after(w, "local step:") == 120  # T-1 = 2 local applies per global step
+    assert "Session from worker 0 closed cleanly" in w
+    # TF-layout checkpoint with the g/ mirror keys and the PS-side Adagrad slots
+    import dtg
+    ck = dtg.train.latest_checkpoint(str(tmp_path / "logdir"))
+    assert ck.endswith("model.ckpt-60")
+    keys = dtg.train.NewCheckpointReader(ck).get_variable_to_shape_map()
+    assert {"global_step", "g/Variable", "g/Variable_1", "g/Variable/Adagrad", "g/Variable_1/Adagrad"} <= set(keys)
+    assert "Variable" not in keys and "local_step" not in keys  # local variables are not saved
+
+
+def test_downpour_resume_stops_immediately(tmp_path):
+    logdir = str(tmp_path / "logdir")
+    _ok(run_cluster("DOWNPOUR/DOWNPOUR.py", 1, 1, ["--logdir", logdir]))
+    out = run_cluster("DOWNPOUR/DOWNPOUR.py", 1, 1, ["--logdir", logdir])
+    _ok(out)
+    w = out[("worker", 0)][1]
+    # restored global_step = 60 >= last_step (absolute): the job stops before any training step
+    assert "global step:" not in w
+    assert "Session from worker 0 closed cleanly" in w
+    import dtg
+    r = dtg.train.NewCheckpointReader(dtg.train.latest_checkpoint(logdir))
+    assert int(r.get_tensor("global_step")) == 60
+
+
+def test_downpour_two_workers(tmp_path):
+    out = run_cluster("DOWNPOUR/DOWNPOUR.py", 1, 2, ["--logdir", str(tmp_path / "l")])
+    _ok(out)
+    steps = [last_int_after(out[("worker", i)][1], "global step:") for i in range(2)]
+    assert max(steps) >= 60
+    c = last_vector(out[("worker", 0)][1], "global step")
+    assert 0.0 < c < 100.0
+
+
+def test_downpour_easy(tmp_path):
+    out = run_cluster("DOWNPOUR-Easy/DOWNPOUR.py", 1, 2, ["--logdir", str(tmp_path / "l")])
+    _ok(out)
+    assert max(last_int_after(out[("worker", i)][1], "global step:") for i in range(2)) >= 60
+
+
+def test_adag_one_worker_oracle(tmp_path):
+    out = run_cluster("ADAG/ADAG.py", 1, 1, ["--logdir", str(tmp_path / "l"), "--debug_window", "0"])
+    _ok(out)
+    w = out[("worker", 0)][1]
+    assert abs(last_vector(w, "global step") - 0.79672914) < 2e-6
+    assert last_int_after(w, "global step:") == 40
+
+
+def test_adag_two_workers_with_debug_prints(tmp_path):
+    out = run_cluster("ADAG/ADAG.py", 1, 2, ["--logdir", str(tmp_path / "l")])
+    _ok(out)
+
+
+def test_ssgd_lockstep_oracle():
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 2, ["--init_tokens", "0"])
+    _ok(out)
+    for i in range(2):
+        w = out[("worker", i)][1]
+        assert abs(last_vector(w, "step:") - 0.1998201) < 2e-6
+        assert last_int_after(w, "step: ") == 10
+
+
+def test_ssgd_tf_token_semantics():
+    """TF default tokens: workers may run one step ahead; accepted run-ahead gradients are computed
+    one step stale, so c lands within a step of the lock-step oracle and global_step hits 10."""
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 2)
+    _ok(out)
+    w = out[("worker", 0)][1]
+    assert abs(last_vector(w, "step:") - 0.1998201) < 2e-4
+    assert last_int_after(w, "step: ") >= 10
+
+
+def test_ssgd_backup_worker_drops_gradients():
+    """3 workers, aggregate 2: the third gradient of each step is a backup (dropped as stale)."""
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 3, ["--init_tokens", "0"])
+    _ok(out)
+    assert last_int_after(out[("worker", 0)][1], "step: ") >= 10
+
+
+def test_ssgd_different_lr_oracle():
+    out = run_cluster("Synchronous-SGD-different-learning-rates/ssgd.py", 1, 2, ["--init_tokens", "0"])
+    _ok(out)
+    assert abs(last_vector(out[("worker", 0)][1], "step:") - 89.289395) < 1e-3
+
+
+def test_sdag_equals_ssgd():
+    out = run_cluster("SDAG/dist_cpu_sing_mach_sync.py", 1, 2, ["--init_tokens", "0"])
+    _ok(out)
+    lines = [l for l in out[("worker", 1)][1].splitlines() if l.startswith("[")]
+    assert abs(float(lines[-1].strip("[").split()[0]) - 0.1998201) < 2e-6
+
+
+def test_hogwild_two_workers(tmp_path):
+    out = run_cluster("Hogwild/Hogwild.py", 1, 2, ["--steps", "300", "--logdir", str(tmp_path / "l")])
+    _ok(out)
+    import re
+    vals = [float(re.search(r"\[\s*([-\d.e+]+)", l).group(1)) for l in out[("worker", 0)][1].splitlines()
+            if l.startswith("[")]
+    assert len(vals) == 30
+    gaps = [100 - v for v in vals]
+    assert all(b <= a + 1e-3 for a, b in zip(gaps, gaps[1:]))  # monotone toward 100
+    import dtg
+    ck = dtg.train.latest_checkpoint(str(tmp_path / "l"))
+    r = dtg.train.NewCheckpointReader(ck)
+    # the chief's final save happens when IT finishes: its 300 applies are in, the other worker's
+    # are in flight (the PS counts every lock-free apply exactly once under the step lock)
+    assert 300 <= int(r.get_tensor("global_step")) <= 600
+
+
+def test_distributed_setup_mts():
+    _ok(run_cluster("Distributed-Setup/dist_setup.py", 1, 1, ["--steps", "50"]))
+
+
+def test_distributed_setup_supervisor(tmp_path):
+    out = run_cluster("Distributed-Setup/dist_setup_sup.py", 1, 1, ["--steps", "50", "--logdir", str(tmp_path / "l")])
+    _ok(out)
+    assert os.path.exists(tmp_path / "l" / "checkpoint")
+
+
+def test_multi_gpu_example_runs_on_cpu(tmp_path):
+    out = run_cluster("Multiple-GPUs-Single-Machine/dist_mult_gpu_sing_mach.py", 1, 2,
+                      ["--steps", "40", "--logdir", str(tmp_path / "l")], env={"HIP_VISIBLE_DEVICES": "-1"})
+    _ok(out)
+
+
+def test_non_distributed_gap_factor():
+    import subprocess
+    import sys
+    from _cluster import ROOT
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "Non-Distributed_Setup.py"), "--observe_sleep",
+                        "0"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    import re
+    vals = [float(re.search(r"\[\s*([-\d.e+]+)", l).group(1)) for l in p.stdout.splitlines() if l.startswith("[")]
+    assert len(vals) == 100
+    ratio = (100 - vals[-1]) / (100 - vals[0])
+    assert abs(ratio - 0.9998 ** 990) < 1e-4  # gap shrinks by (1 - 2 lr) per step; it does not converge
