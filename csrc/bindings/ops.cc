@@ -278,9 +278,77 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
                  cur_stream());
 }
 
+// ---- implicit-GEMM convolution -----------------------------------------------------------------
+// Activations are NHWC-contiguous ("channels_last") bf16 tensors given as [N, H, W, C] views;
+// the weight is [K, R, S, C] contiguous (a channels_last [K, C, R, S] parameter viewed as such).
+void check_nhwc(const Tensor& t, const char* what) {
+  CHECK_CUDA(t);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, what, " must be bf16");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(), what, " must be a contiguous [N,H,W,C] tensor");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() % 16) == 0, what, " must be 16-byte aligned");
+}
+
+bool conv_supported(int64_t C, int64_t K, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t which) {
+  return dtg::conv_supported((int)C, (int)K, (int)R, (int)S, (int)stride, (int)pad, (int)which) != 0;
+}
+
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "weight channels mismatch");
+  TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 0), "conv shape not supported by the HIP kernel");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty output");
+  TORCH_CHECK((long long)N * H * W * C < (1LL << 31) && (long long)N * P * Q * K < (1LL << 31), "tensor too large");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, P, Q, K}, x.options());
+  dtg::conv_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, C, K, R, S, stride, pad, cur_stream());
+  return y;
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+  check_nhwc(dy, "dy");
+  check_nhwc(w, "w");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  const int R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(w.size(0) == K, "weight/dy channel mismatch");
+  TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 1), "dgrad shape not supported by the HIP kernel");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q, "dgrad geometry mismatch");
+  c10::DeviceGuard dg(dy.device());
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, cur_stream());
+  return dx;
+}
+
+// dw (+)= wgrad; dw is [K, R, S, C] contiguous, fp32 or bf16 (beta = 1 accumulates into a flat grad)
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad) {
+  check_nhwc(dy, "dy");
+  check_nhwc(x, "x");
+  CHECK_CUDA(dw);
+  TORCH_CHECK(dw.dim() == 4 && dw.is_contiguous(), "dw must be contiguous [K,R,S,C]");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat || dw.scalar_type() == at::kBFloat16, "dw fp32/bf16");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = dw.size(0), R = dw.size(1), S = dw.size(2);
+  TORCH_CHECK(dw.size(3) == C && dy.size(3) == K && dy.size(0) == N, "wgrad shape mismatch");
+  TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 2), "wgrad shape not supported by the HIP kernel");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dy.size(1) == P && dy.size(2) == Q, "wgrad geometry mismatch");
+  c10::DeviceGuard dg(x.device());
+  const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad);
+  auto ws = at::empty({(long long)split * K * R * S * C}, x.options().dtype(at::kFloat));
+  dtg::conv_wgrad(cbfp(dy), cbfp(x), dw.data_ptr(), dw.scalar_type() == at::kBFloat16, (float)beta,
+                  ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("conv_supported", &conv_supported);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);
   m.def("momentum_apply", &momentum_apply);

@@ -1,0 +1,61 @@
+// Shared GEMM epilogue: C = act(alpha * acc + beta * C + bias), fp32 or bf16 output, 8 columns
+// at a time (16-byte vectors when aligned).  Used by gemm.hip and conv.hip.
+#pragma once
+#include "dtg/common.h"
+
+namespace dtg {
+
+struct Epi {
+  void* C;
+  long long ldc;
+  int c_bf16;
+  float alpha, beta;
+  const float* bias;  // per column (N), may be null
+  int act;            // 0 none, 1 relu, 2 gelu(tanh)
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) {
+    const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
+    return 0.5f * v * (1.f + tanhf(u));
+  }
+  return v;
+}
+
+// finish 8 consecutive columns [n, n+8) of row m (n < N; the tail is masked element-wise)
+__device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, float (&v)[8]) {
+  const long long off = (long long)m * e.ldc + n;
+  const int cnt = N - n < 8 ? N - n : 8;
+  const bool vec = cnt == 8 && ((e.ldc & 7) == 0);
+  float old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (e.beta != 0.f) {
+    if (vec) {
+      if (e.c_bf16) load8_bf16((const bf16_t*)e.C + off, old);
+      else load8_f32((const float*)e.C + off, old);
+    } else {
+      for (int k = 0; k < cnt; ++k)
+        old[k] = e.c_bf16 ? bf2f(((const bf16_t*)e.C)[off + k]) : ((const float*)e.C)[off + k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float x = v[k] * e.alpha + e.beta * old[k];
+    if (e.bias && k < cnt) x += e.bias[n + k];
+    v[k] = apply_act(x, e.act);
+  }
+  if (vec) {
+    if (e.c_bf16) store8_bf16((bf16_t*)e.C + off, v);
+    else store8_f32((float*)e.C + off, v);
+  } else {
+    for (int k = 0; k < cnt; ++k) {
+      if (e.c_bf16) ((bf16_t*)e.C)[off + k] = f2bf(v[k]);
+      else ((float*)e.C)[off + k] = v[k];
+    }
+  }
+}
+
+// split-K reduction of fp32 slabs [split][M][N] + the epilogue (gemm.hip)
+void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st);
+
+}  // namespace dtg

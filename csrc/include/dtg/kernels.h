@@ -46,4 +46,15 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st);
 
+// ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
+// which: 0 fwd, 1 dgrad, 2 wgrad
+int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
+void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
+              int stride, int pad, hipStream_t st);
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
+                int stride, int pad, hipStream_t st);
+int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad);
+void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st);
+
 }  // namespace dtg

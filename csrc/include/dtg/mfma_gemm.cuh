@@ -188,10 +188,12 @@ __device__ __forceinline__ void compute_tile(const lds_char* At, const lds_char*
 }
 
 // ---- main loop -------------------------------------------------------------------------------
-// Accumulates the K range [kbeg, kend) of tile (bm0, bn0) into acc[4][4].
-template <class C, bool AKC, bool BKC, class SA, class SB>
-__device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* smem, int bm0, int bn0, int kbeg,
-                                         int kend, f32x4 (&acc)[4][4]) {
+// Accumulates the K range [kbeg, kend) into acc[4][4].  STA(tile, k0) / STB(tile, k0) issue the
+// LDS-DMA of one 64-deep K-step of the A / B operand into an LDS tile (generic stagers below,
+// or implicit-GEMM gathers in conv.hip).
+template <class C, bool AKC, bool BKC, class STA, class STB>
+__device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_char* smem, int kbeg, int kend,
+                                            f32x4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
@@ -199,23 +201,23 @@ __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* s
   if (nk <= 0) return;
   if constexpr (C::STAGES == 1) {
     for (int kt = 0; kt < nk; ++kt) {
-      stage<AKC, C::BM>(sa, smem, bm0, kbeg + kt * BK, wave, lane);
-      stage<BKC, C::BN>(sb, smem + C::A_BYTES, bn0, kbeg + kt * BK, wave, lane);
+      sta(smem, kbeg + kt * BK);
+      stb(smem + C::A_BYTES, kbeg + kt * BK);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       compute_tile<C, AKC, BKC>(smem, smem + C::A_BYTES, wm, wn, lane, acc);
       __syncthreads();
     }
   } else {
-    stage<AKC, C::BM>(sa, smem, bm0, kbeg, wave, lane);
-    stage<BKC, C::BN>(sb, smem + C::A_BYTES, bn0, kbeg, wave, lane);
+    sta(smem, kbeg);
+    stb(smem + C::A_BYTES, kbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = (kt & 1) * C::STAGE_BYTES, nxt = C::STAGE_BYTES - cur;
       if (kt + 1 < nk) {
-        stage<AKC, C::BM>(sa, smem + nxt, bm0, kbeg + (kt + 1) * BK, wave, lane);
-        stage<BKC, C::BN>(sb, smem + nxt + C::A_BYTES, bn0, kbeg + (kt + 1) * BK, wave, lane);
+        sta(smem + nxt, kbeg + (kt + 1) * BK);
+        stb(smem + nxt + C::A_BYTES, kbeg + (kt + 1) * BK);
       }
       compute_tile<C, AKC, BKC>(smem + cur, smem + cur + C::A_BYTES, wm, wn, lane, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -223,6 +225,34 @@ __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* s
     }
   }
 }
+
+template <class C, bool AKC, bool BKC, class SA, class SB>
+__device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* smem, int bm0, int bn0, int kbeg,
+                                         int kend, f32x4 (&acc)[4][4]) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  mainloop_st<C, AKC, BKC>([&](lds_char* t, int k0) { stage<AKC, C::BM>(sa, t, bm0, k0, wave, lane); },
+                           [&](lds_char* t, int k0) { stage<BKC, C::BN>(sb, t, bn0, k0, wave, lane); }, smem, kbeg,
+                           kend, acc);
+}
+
+// ---- fast integer division by a runtime constant (Granlund-Montgomery), n < 2^31 --------------
+struct FastDiv {
+  uint32_t d, m, l;
+  FastDiv() : d(1), m(1), l(0) {}
+  explicit FastDiv(uint32_t dd) : d(dd) {
+    l = 0;
+    while ((1u << l) < d) ++l;
+    m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> l);
+  }
+  __device__ __forceinline__ void divmod(uint32_t n, uint32_t& q, uint32_t& r) const {
+    q = div(n);
+    r = n - q * d;
+  }
+};
 
 // ---- epilogue ----------------------------------------------------------------------------------
 // Stages the block's fp32 accumulators through LDS (EPI_ROWS rows at a time) so that every

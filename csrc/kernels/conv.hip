@@ -1,0 +1,315 @@
+// Implicit-GEMM 2-D convolution, NHWC bf16, on the MFMA GEMM core (dtg/mfma_gemm.cuh).
+// No im2col buffer: each lane's LDS-DMA source address IS the gather (the glds global address is
+// per lane), so the "im2col" matrix only ever exists as 16-byte chunks in flight.
+//
+//   x  [N, H, W, C]     w [K, R, S, C]  (= a channels_last [K, C, R, S] parameter)    y [N, P, Q, K]
+//
+//   fwd    y[(n,p,q), k]      = sum_{(r,s,c)} x[n, p*st-pad+r, q*st-pad+s, c] * w[k, r, s, c]
+//          A: gather of x (K-contiguous chunks of 8 channels)          B: w, dense K-contiguous
+//   dgrad  dx[(n,h,w), c]     = sum_{(r,s,k)} dy[n, h+pad-r, w+pad-s, k] * w[k, r, s, c]     (stride 1)
+//          A: gather of dy (K-contiguous)                              B: gather of w, MN-contiguous
+//   wgrad  dw[k, (r,s,c)]     = sum_{(n,p,q)} dy[(n,p,q), k] * x[n, p*st-pad+r, q*st-pad+s, c]
+//          A: dy, dense MN-contiguous                                  B: gather of x, MN-contiguous
+//          split over (n,p,q) with fp32 slabs + a reduce pass that accumulates into the flat grad.
+// Requirements (checked on the host): C % 64 == 0 and K % 64 == 0 (a 64-deep K-step then stays inside
+// one filter tap, so the tap is uniform per step and only the row/channel part is per lane).
+// Out-of-image taps read the zero page; row/column clamps keep every address inside its tensor.
+#include "dtg/common.h"
+#include "dtg/gemm_epi.cuh"
+#include "dtg/kernels.h"
+#include "dtg/mfma_gemm.cuh"
+
+namespace dtg {
+using namespace gemm;
+
+struct ConvGeom {
+  int N, H, W, C, K, R, S, P, Q, stride, pad;
+  FastDiv fPQ, fQ, fHW, fW, fC, fS, fK;
+};
+
+static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
+  g.P = (H + 2 * pad - R) / stride + 1;
+  g.Q = (W + 2 * pad - S) / stride + 1;
+  g.fPQ = FastDiv(g.P * g.Q); g.fQ = FastDiv(g.Q); g.fHW = FastDiv(H * W); g.fW = FastDiv(W);
+  g.fC = FastDiv(C); g.fS = FastDiv(S); g.fK = FastDiv(K);
+  return g;
+}
+
+// ---- fwd A: x gathered at the output positions of the tile rows (KC) ---------------------------
+template <int ROWS>
+struct FwdA {
+  static constexpr int PW = ROWS / 32;
+  const bf16_t* x;
+  const ConvGeom* g;
+  int nbase[PW], ih0[PW], iw0[PW];
+  int cx;  // this lane's source chunk (0..7) -- constant: (lane & 7) ^ (row & 7) with row & 7 = lane >> 3
+  __device__ __forceinline__ void init(const ConvGeom& G, const bf16_t* xp, int row0, int wave, int lane) {
+    x = xp;
+    g = &G;
+    const int M = G.N * G.P * G.Q;
+    cx = (lane & 7) ^ (lane >> 3);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      int m = row0 + (wave * PW + i) * 8 + (lane >> 3);
+      m = m < M ? m : M - 1;
+      uint32_t n, pq, p, q;
+      G.fPQ.divmod((uint32_t)m, n, pq);
+      G.fQ.divmod(pq, p, q);
+      nbase[i] = (int)n * G.H;
+      ih0[i] = (int)p * G.stride - G.pad;
+      iw0[i] = (int)q * G.stride - G.pad;
+    }
+  }
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave) const {
+    uint32_t rs, c0, r, s;
+    g->fC.divmod((uint32_t)k0, rs, c0);
+    g->fS.divmod(rs, r, s);
+    const int ch = (int)c0 + cx * 8;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int ih = ih0[i] + (int)r, iw = iw0[i] + (int)s;
+      const bool ok = (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
+      const int ihc = ok ? ih : 0, iwc = ok ? iw : 0;
+      const void* src = sel(ok, x + ((long long)(nbase[i] + ihc) * g->W + iwc) * g->C + ch);
+      const int r0 = (wave * PW + i) * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + r0 * 128), 16, 0, 0);
+    }
+  }
+};
+
+// ---- dgrad A: dy gathered at the input positions of the tile rows (KC), stride 1 ----------------
+template <int ROWS>
+struct DgradA {
+  static constexpr int PW = ROWS / 32;
+  const bf16_t* dy;
+  const ConvGeom* g;
+  int nbase[PW], ph0[PW], qw0[PW];
+  int cx;
+  __device__ __forceinline__ void init(const ConvGeom& G, const bf16_t* dyp, int row0, int wave, int lane) {
+    dy = dyp;
+    g = &G;
+    const int M = G.N * G.H * G.W;
+    cx = (lane & 7) ^ (lane >> 3);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      int m = row0 + (wave * PW + i) * 8 + (lane >> 3);
+      m = m < M ? m : M - 1;
+      uint32_t n, hw, h, w;
+      G.fHW.divmod((uint32_t)m, n, hw);
+      G.fW.divmod(hw, h, w);
+      nbase[i] = (int)n * G.P;
+      ph0[i] = (int)h + G.pad;
+      qw0[i] = (int)w + G.pad;
+    }
+  }
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave) const {
+    uint32_t rs, k0c, r, s;
+    g->fK.divmod((uint32_t)k0, rs, k0c);
+    g->fS.divmod(rs, r, s);
+    const int ch = (int)k0c + cx * 8;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int p = ph0[i] - (int)r, q = qw0[i] - (int)s;
+      const bool ok = (unsigned)p < (unsigned)g->P && (unsigned)q < (unsigned)g->Q;
+      const int pc = ok ? p : 0, qc = ok ? q : 0;
+      const void* src = sel(ok, dy + ((long long)(nbase[i] + pc) * g->Q + qc) * g->K + ch);
+      const int r0 = (wave * PW + i) * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + r0 * 128), 16, 0, 0);
+    }
+  }
+};
+
+// ---- dgrad B: w as B[(r,s,k)][c] (MC: c contiguous) ---------------------------------------------
+template <int ROWS>
+struct DgradB {
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  const bf16_t* w;
+  const ConvGeom* g;
+  int col0;
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave, int lane) const {
+    uint32_t rs, kb;
+    g->fK.divmod((uint32_t)k0, rs, kb);
+    const long long rsc = (long long)g->R * g->S * g->C;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int kr0 = (wave * PW + i) * KPI;
+      const int kr = kr0 + lane / CH;
+      const int c = (lane % CH) ^ mc_swz<CH>(kr);
+      const int col = col0 + c * 8;
+      const bool ok = col < g->C;
+      const void* src = sel(ok, w + (long long)((int)kb + kr) * rsc + (long long)rs * g->C + (ok ? col : 0));
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + kr0 * ROWS * 2), 16, 0, 0);
+    }
+  }
+};
+
+// ---- wgrad B: x as B[(n,p,q)][(r,s,c)] (MC: c contiguous) ----------------------------------------
+template <int ROWS>
+struct WgradB {
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  const bf16_t* x;
+  const ConvGeom* g;
+  int col0, M;
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave, int lane) const {
+    const int ncols = g->R * g->S * g->C;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int kr0 = (wave * PW + i) * KPI;
+      const int kr = kr0 + lane / CH;
+      const int c = (lane % CH) ^ mc_swz<CH>(kr);
+      const int col = col0 + c * 8;
+      const int m = k0 + kr;
+      uint32_t n, pq, p, q, rs, cc, r, s;
+      g->fPQ.divmod((uint32_t)(m < M ? m : 0), n, pq);
+      g->fQ.divmod(pq, p, q);
+      g->fC.divmod((uint32_t)(col < ncols ? col : 0), rs, cc);
+      g->fS.divmod(rs, r, s);
+      const int ih = (int)p * g->stride - g->pad + (int)r, iw = (int)q * g->stride - g->pad + (int)s;
+      const bool ok = m < M && col < ncols && (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
+      const void* src = sel(ok, x + ((long long)((int)n * g->H + (ok ? ih : 0)) * g->W + (ok ? iw : 0)) * g->C + cc);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + kr0 * ROWS * 2), 16, 0, 0);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+template <class CF>
+__global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int M = G.N * G.P * G.Q, Kd = G.R * G.S * G.C;
+  FwdA<CF::BM> sa;
+  sa.init(G, x, bm0, wave, lane);
+  DenseKC<false> sb{w, (long long)Kd, G.K, Kd};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mainloop_st<CF, true, true>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
+                              [&](lds_char* tl, int k0) { stage_kc<CF::BN>(sb, tl, bn0, k0, wave, lane); }, smem, 0,
+                              Kd, acc);
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.K, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.K, m, n, v); });
+}
+
+template <class CF>
+__global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int M = G.N * G.H * G.W, Kd = G.R * G.S * G.K;
+  DgradA<CF::BM> sa;
+  sa.init(G, dy, bm0, wave, lane);
+  DgradB<CF::BN> sb{w, &G, bn0};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
+                               [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.C, m, n, v); });
+}
+
+template <class CF>
+__global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
+                                                           const bf16_t* __restrict__ x, float* __restrict__ ws,
+                                                           int tiles_n, int k_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int M = G.N * G.P * G.Q;              // reduction length
+  const int Mo = G.K, No = G.R * G.S * G.C;   // output dw [K][RSC]
+  const int kbeg = blockIdx.y * k_per_split, kend = min(M, kbeg + k_per_split);
+  DenseMC<true> sa{dy, (long long)G.K, G.K, M};
+  WgradB<CF::BN> sb{x, &G, bn0, M};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mainloop_st<CF, false, false>([&](lds_char* tl, int k0) { stage_mc<CF::BM>(sa, tl, bm0, k0, wave, lane); },
+                                [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, kbeg, kend, acc);
+  float* slab = ws + (long long)blockIdx.y * Mo * No;
+  epilogue_staged<CF>(smem, acc, bm0, bn0, Mo, No, [&](int m, int n, float (&v)[8]) {
+    store8_f32(slab + (long long)m * No + n, v);
+  });
+}
+
+// ---------------------------------------------------------------------------------------------
+static bool conv_skinny(int n) { return n <= 64; }
+
+int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
+  if (C % 64 || K % 64) return 0;
+  if (which == 1 && stride != 1) return 0;  // dgrad: stride-1 only (strided dgrad -> library)
+  return 1;
+}
+
+void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
+              int stride, int pad, hipStream_t st) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+  const int M = N * G.P * G.Q;
+  Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
+  if (conv_skinny(K)) {
+    using CF = Cfg<256, 64, 2>;
+    const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn);
+  } else {
+    using CF = Cfg<128, 128, 2>;
+    const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn);
+  }
+}
+
+void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
+                int stride, int pad, hipStream_t st) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+  const int M = N * H * W;
+  Epi e{dx, C, 1, 1.f, 0.f, nullptr, 0};
+  if (conv_skinny(C)) {
+    using CF = Cfg<256, 64, 2>;
+    const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn);
+  } else {
+    using CF = Cfg<128, 128, 2>;
+    const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn);
+  }
+}
+
+int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+  const int M = N * G.P * G.Q, No = R * S * C;
+  const long long tiles = (long long)((K + 127) / 128) * ((No + 127) / 128);
+  int s = 1;
+  while (tiles * s < 512 && (long long)M / (s * 2) >= 1024 && s < 256) s *= 2;
+  return s;
+}
+
+void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+  const int M = N * G.P * G.Q, No = R * S * C;
+  int kps = (M + split - 1) / split;
+  kps = (kps + BK - 1) / BK * BK;
+  split = (M + kps - 1) / kps;
+  using CF = Cfg<128, 128, 2>;
+  const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
+  dim3 grid(tm * tn, split);
+  conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
+  Epi e{dw, No, dw_bf16, 1.f, beta, nullptr, 0};
+  gemm_splitk_reduce(ws, split, K, No, e, st);
+}
+
+}  // namespace dtg

@@ -9,60 +9,11 @@
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
+#include "dtg/gemm_epi.cuh"
 #include <type_traits>
 
 namespace dtg {
 using namespace gemm;
-
-struct Epi {
-  void* C;
-  long long ldc;
-  int c_bf16;
-  float alpha, beta;
-  const float* bias;  // per column (N), may be null
-  int act;            // 0 none, 1 relu, 2 gelu(tanh)
-};
-
-__device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == 1) return fmaxf(v, 0.f);
-  if (act == 2) {
-    const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
-    return 0.5f * v * (1.f + tanhf(u));
-  }
-  return v;
-}
-
-// finish 8 consecutive columns [n, n+8) of row m (n < N; the tail is masked element-wise)
-__device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, float (&v)[8]) {
-  const long long off = (long long)m * e.ldc + n;
-  const int cnt = N - n < 8 ? N - n : 8;
-  const bool vec = cnt == 8 && ((e.ldc & 7) == 0);
-  float old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (e.beta != 0.f) {
-    if (vec) {
-      if (e.c_bf16) load8_bf16((const bf16_t*)e.C + off, old);
-      else load8_f32((const float*)e.C + off, old);
-    } else {
-      for (int k = 0; k < cnt; ++k)
-        old[k] = e.c_bf16 ? bf2f(((const bf16_t*)e.C)[off + k]) : ((const float*)e.C)[off + k];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float x = v[k] * e.alpha + e.beta * old[k];
-    if (e.bias && k < cnt) x += e.bias[n + k];
-    v[k] = apply_act(x, e.act);
-  }
-  if (vec) {
-    if (e.c_bf16) store8_bf16((bf16_t*)e.C + off, v);
-    else store8_f32((float*)e.C + off, v);
-  } else {
-    for (int k = 0; k < cnt; ++k) {
-      if (e.c_bf16) ((bf16_t*)e.C)[off + k] = f2bf(v[k]);
-      else ((float*)e.C)[off + k] = v[k];
-    }
-  }
-}
 
 template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
@@ -206,6 +157,16 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   }
 }
 
+void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
+  if (N % 8 == 0) {
+    const long long plane = (long long)M * N;
+    splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e);
+  } else {
+    const long long total = (long long)M * ((N + 7) / 8);
+    splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
+  }
+}
+
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st) {
@@ -219,15 +180,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act};
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  if (split_k > 1) {
-    if (N % 8 == 0) {
-      const long long plane = (long long)M * N;
-      splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e);
-    } else {
-      const long long total = (long long)M * ((N + 7) / 8);
-      splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
-    }
-  }
+  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 
 }  // namespace dtg

@@ -1,10 +1,12 @@
-"""2-D convolution on NHWC (channels_last) bf16 activations.
+"""2-D convolution on NHWC (channels_last) bf16 activations -- dtg's own MFMA kernels.
 
-Dispatch (set ``DTG_CONV_IMPL=miopen`` to force the library path for A/B runs):
-  * 1x1 / stride 1 / pad 0  -> the MFMA GEMM (csrc/kernels/gemm.hip) on the [N*H*W, C] row view:
+Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
+  * 1x1 / stride 1 / pad 0 -> the MFMA GEMM (csrc/kernels/gemm.hip) on the [N*H*W, C] row view:
         fwd  Y  = X  W^T      dgrad dX = dY W      wgrad dW = dY^T X
-  * k x k implicit-GEMM     -> csrc/kernels/conv.hip when built with it (see ``_IMPLICIT``)
-  * everything else         -> MIOpen through torch (stem 7x7/Cin=3 etc.)
+  * k x k, C % 64 == 0, K % 64 == 0 -> implicit-GEMM conv (csrc/kernels/conv.hip):
+        fwd and wgrad at any stride, dgrad at stride 1 (strided dgrad -> MIOpen)
+  * everything else (the 7x7/Cin=3 stem) -> MIOpen through torch
+Weight gradients are accumulated straight into the flat gradient buffer (see parallel/grad_sink).
 """
 import os
 
@@ -12,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from ..parallel import grad_sink
+from ._native import lib
 from .gemm import gemm
 
 _IMPL = os.environ.get("DTG_CONV_IMPL", "dtg")
@@ -24,14 +27,20 @@ def _rows(t):
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
+def _nhwc(t):
+    if not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    return t.permute(0, 2, 3, 1)
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         n, c, h, wd = x.shape
         cout = w.shape[0]
         x2 = _rows(x)
-        w2 = w.as_strided((cout, c), (c, 1)) if w.is_contiguous(memory_format=torch.channels_last) or w.is_contiguous() \
-            else w.reshape(cout, c).contiguous()
+        w2 = w.as_strided((cout, c), (c, 1)) if (w.is_contiguous(memory_format=torch.channels_last)
+                                                  or w.is_contiguous()) else w.reshape(cout, c).contiguous()
         y2 = gemm(x2, True, w2, True)
         ctx.save_for_backward(x2, w2)
         ctx.shape = (n, c, h, wd)
@@ -56,9 +65,48 @@ class _Conv1x1(torch.autograd.Function):
         return dx, dw2.view(ctx.wshape)
 
 
+class _ConvImplicit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        x4 = _nhwc(x)
+        w4 = _nhwc(w)  # [K, R, S, C]
+        y4 = lib().conv_fwd(x4.contiguous(), w4.contiguous(), stride, pad)
+        ctx.save_for_backward(x4, w4)
+        ctx.stride, ctx.pad = stride, pad
+        ctx.xshape, ctx.w = x.shape, w
+        ctx.param = w if grad_sink.enabled(w) else None
+        return y4.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x4, w4 = ctx.saved_tensors
+        st, pad = ctx.stride, ctx.pad
+        dy4 = _nhwc(dy).contiguous()
+        n, c, h, wd = ctx.xshape
+        k, r, s = w4.shape[0], w4.shape[1], w4.shape[2]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if lib().conv_supported(c, k, r, s, st, pad, 1):
+                dx = lib().conv_dgrad(dy4, w4.contiguous(), h, wd, st, pad).permute(0, 3, 1, 2)
+            else:  # strided dgrad: MIOpen
+                w_cl = w4.permute(0, 3, 1, 2)
+                dx = torch.nn.grad.conv2d_input(ctx.xshape, w_cl, dy4.permute(0, 3, 1, 2), st, pad)
+        p = ctx.param
+        if p is not None:
+            lib().conv_wgrad(dy4, x4.contiguous(), p.grad.permute(0, 2, 3, 1), 1.0, st, pad)
+            grad_sink.notify(p)
+            return dx, None, None, None
+        dw4 = torch.empty_like(w4.contiguous())
+        lib().conv_wgrad(dy4, x4.contiguous(), dw4, 0.0, st, pad)
+        return dx, dw4.permute(0, 3, 1, 2), None, None
+
+
 def conv2d(x, w, stride=1, padding=0):
     kh, kw = w.shape[2], w.shape[3]
-    if (_IMPL == "dtg" and x.is_cuda and x.dtype == torch.bfloat16 and kh == 1 and kw == 1 and stride == 1
-            and padding == 0 and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0):
-        return _Conv1x1.apply(x, w)
+    cin, cout = x.shape[1], w.shape[0]
+    if _IMPL == "dtg" and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
+        if kh == 1 and kw == 1 and stride == 1 and padding == 0 and cin % 8 == 0 and cout % 8 == 0:
+            return _Conv1x1.apply(x, w)
+        if cin % 64 == 0 and cout % 64 == 0:
+            return _ConvImplicit.apply(x, w, stride, padding)
     return F.conv2d(x, w, None, stride, padding)
