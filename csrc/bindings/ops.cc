@@ -177,9 +177,11 @@ Tensor bn_fwd_infer(Tensor x, c10::optional<Tensor> res, Tensor gamma, Tensor be
   return y;
 }
 
+// dgamma_acc / dbeta_acc given: the parameter gradients are ACCUMULATED into them (flat grads)
 std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd(Tensor dy, c10::optional<Tensor> y, Tensor x,
                                                                   Tensor gamma, Tensor smean, Tensor sinv, bool relu,
-                                                                  bool want_dres) {
+                                                                  bool want_dres, c10::optional<Tensor> dgamma_acc,
+                                                                  c10::optional<Tensor> dbeta_acc) {
   CHECK_IN(dy);
   CHECK_IN(x);
   CHECK_DT(dy, at::kBFloat16);
@@ -203,11 +205,24 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd(Tensor dy, c10:
   c10::optional<Tensor> dres;
   if (want_dres) dres = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
-  auto dgamma = at::empty({C}, fopt), dbeta = at::empty({C}, fopt);
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined() && dbeta_acc.has_value() && dbeta_acc->defined();
+  Tensor dgamma, dbeta;
+  if (acc) {
+    dgamma = *dgamma_acc;
+    dbeta = *dbeta_acc;
+    for (const Tensor* t : {&dgamma, &dbeta}) {
+      CHECK_IN(*t);
+      CHECK_DT(*t, at::kFloat);
+      TORCH_CHECK(t->numel() == C, "gradient accumulator size mismatch");
+    }
+  } else {
+    dgamma = at::empty({C}, fopt);
+    dbeta = at::empty({C}, fopt);
+  }
   auto ws = at::empty({dtg::bn_workspace_floats(M, C) + C}, fopt);
   dtg::bn_bwd(cbfp(dy), relu ? cbfp(*y) : nullptr, cbfp(x), gamma.data_ptr<float>(), smean.data_ptr<float>(),
               sinv.data_ptr<float>(), bfp(dx), want_dres ? bfp(*dres) : nullptr, dgamma.data_ptr<float>(),
-              dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu, cur_stream());
+              dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, relu, acc, cur_stream());
   return {dx, dres, dgamma, dbeta};
 }
 
@@ -358,7 +373,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_infer", &bn_fwd_infer);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, pybind11::arg("dy"), pybind11::arg("y"), pybind11::arg("x"), pybind11::arg("gamma"),
+        pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("relu"), pybind11::arg("want_dres"),
+        pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("softmax_xent", &softmax_xent);
   m.def("gemm", &gemm);
 }

@@ -33,7 +33,7 @@ void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
                   hipStream_t st);
 void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gamma, const float* smean,
             const float* sinv, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M, int C,
-            int relu, hipStream_t st);
+            int relu, int accum, hipStream_t st);
 
 // ---- softmax cross-entropy (softmax_xent.hip) ------------------------------------------------
 void softmax_xent(const void* x, int x_bf16, const long long* label, long long B, int V, float scale, float* loss,

@@ -156,8 +156,9 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
     coef[c] = a;
     coef[C + c] = bx;
     coef[2 * C + c] = c0;
-    if (dgamma) dgamma[c] = (float)q;
-    if (dbeta) dbeta[c] = (float)s;
+    // mode 2 accumulates into persistent (flat-buffer) gradients instead of overwriting
+    if (dgamma) dgamma[c] = (mode == 2 ? dgamma[c] : 0.f) + (float)q;
+    if (dbeta) dbeta[c] = (mode == 2 ? dbeta[c] : 0.f) + (float)s;
   }
 }
 
@@ -337,7 +338,7 @@ void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
 
 void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gamma, const float* smean,
             const float* sinv, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M, int C,
-            int relu, hipStream_t st) {
+            int relu, int accum, hipStream_t st) {
   const BnGeom g = bn_geom(M, C);
   float* part = ws;
   float* coef = ws + (long long)g.nchunk * 2 * C;
@@ -346,7 +347,7 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
     if (relu) bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
     else bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
   });
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 1, gamma, nullptr, nullptr, nullptr,
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr, nullptr,
                                                     const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
                                                     coef, dgamma, dbeta);
   DTG_TPR_SWITCH(g.tpr, {

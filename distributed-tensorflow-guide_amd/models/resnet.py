@@ -9,6 +9,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import resnet_fused
 from .layers import ConvBN, Linear
 
 
@@ -23,7 +24,11 @@ class Bottleneck(nn.Module):
         self.c3 = ConvBN(width, cout, 1, zero_init=True)
         self.down = ConvBN(cin, cout, 1, stride) if (stride != 1 or cin != cout) else None
 
+    fused = True  # one autograd node with a hand-written backward on GPU (resnet_fused.py)
+
     def forward(self, x):
+        if self.fused and resnet_fused.fused_ok(self, x):
+            return resnet_fused.bottleneck(self, x)
         idn = self.down(x, relu=False) if self.down is not None else x
         y = self.c1(x)
         y = self.c2(y)

@@ -1,0 +1,157 @@
+"""ResNet bottleneck as ONE autograd node with a hand-written backward (GPU, bf16, NHWC).
+
+Everything runs on dtg's HIP kernels on [rows, channels] views of NHWC activations:
+
+  forward   y1 = x W1^T (MFMA GEMM)        a1 = relu(bn1(y1))             (fused BN+ReLU)
+            y2 = conv3x3(a1, W2, stride)  a2 = relu(bn2(y2))             (implicit-GEMM conv)
+            y3 = a2 W3^T                  idn = x | bn_d(conv1x1_s(x, Wd))
+            out = relu(bn3(y3) + idn)                                     (fused BN+add+ReLU)
+  backward  the residual gradient that BN3's backward emits (dres) is the buffer the first
+            conv's dgrad GEMM accumulates into (beta = 1): the "x is used twice" gradient sum
+            costs no separate add kernel; conv weight gradients are accumulated straight into
+            the flat gradient buffer and BN gamma/beta gradients are accumulated in the BN
+            finalize kernel -- autograd sees no parameter gradients at all, the all-reduce
+            buckets are notified through parallel/grad_sink.
+Strided 3x3 dgrad goes to MIOpen (channels_last, no layout conversion).
+"""
+import torch
+
+from ..ops._native import lib
+from ..ops.gemm import gemm
+from ..parallel import grad_sink
+
+
+def _rows(t):
+    n, c, h, w = t.shape
+    if not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _mat(w):  # 1x1 conv weight [K, C, 1, 1] -> [K, C]
+    return w.reshape(w.shape[0], w.shape[1]) if w.is_contiguous() else w.as_strided((w.shape[0], w.shape[1]),
+                                                                                     (w.shape[1], 1))
+
+
+def _krsc(w):  # channels_last [K, C, R, S] -> contiguous [K, R, S, C] view
+    return w.permute(0, 2, 3, 1)
+
+
+def _gacc(p):
+    """The buffer a parameter's gradient is accumulated into (its flat view, or a fresh one)."""
+    if grad_sink.enabled(p):
+        return p.grad, True
+    return torch.zeros_like(p, dtype=torch.float32 if p.dim() <= 1 else p.dtype), False
+
+
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        L = lib()
+        n, c, h, w = x.shape
+        st = blk.c2.conv.stride
+        width = blk.c1.conv.weight.shape[0]
+        cout = blk.c3.conv.weight.shape[0]
+        x2 = _rows(x)
+        p_, q_ = (h + 2 - 3) // st + 1, (w + 2 - 3) // st + 1
+        b1, b2, b3 = blk.c1.bn, blk.c2.bn, blk.c3.bn
+        w1, w2, w3 = blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight
+        y1 = gemm(x2, True, _mat(w1), True)
+        a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
+                                    b1.eps, True)
+        y2 = L.conv_fwd(a1.view(n, h, w, width), _krsc(w2), st, 1).view(-1, width)
+        a2, m2, i2 = L.bn_fwd_train(y2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.momentum,
+                                    b2.eps, True)
+        y3 = gemm(a2, True, _mat(w3), True)
+        yd = md = idd = None
+        if blk.down is not None:
+            bd, wd = blk.down.bn, blk.down.conv.weight
+            if st == 1:
+                yd = gemm(x2, True, _mat(wd), True)
+            else:
+                yd = L.conv_fwd(x2.view(n, h, w, c), _krsc(wd), st, 0).view(-1, cout)
+            idn, md, idd = L.bn_fwd_train(yd, None, bd.weight, bd.bias, bd.running_mean, bd.running_var, bd.momentum,
+                                          bd.eps, False)
+        else:
+            idn = x2
+        out, m3, i3 = L.bn_fwd_train(y3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.momentum,
+                                     b3.eps, True)
+        ctx.blk = blk
+        ctx.geom = (n, c, h, w, st, width, cout, p_, q_)
+        ctx.save_for_backward(x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3,
+                              *((yd, md, idd) if yd is not None else ()))
+        return out.view(n, p_, q_, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        L = lib()
+        blk = ctx.blk
+        n, c, h, w, st, width, cout, p_, q_ = ctx.geom
+        sv = ctx.saved_tensors
+        x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3 = sv[:13]
+        b1, b2, b3 = blk.c1.bn, blk.c2.bn, blk.c3.bn
+        w1, w2, w3 = blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight
+        params = [w1, b1.weight, b1.bias, w2, b2.weight, b2.bias, w3, b3.weight, b3.bias]
+        if blk.down is not None:
+            params += [blk.down.conv.weight, blk.down.bn.weight, blk.down.bn.bias]
+        accs = [_gacc(p) for p in params]
+        g = {id(p): a for p, (a, _) in zip(params, accs)}
+        do = _rows(dout)
+        # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
+        dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)], g[id(b3.bias)])
+        # conv3 (1x1)
+        da2 = gemm(dy3, True, _mat(w3), False)
+        gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
+        # BN2 + conv2 (3x3)
+        dy2, _, _, _ = L.bn_bwd(da2, a2, y2, b2.weight, m2, i2, True, False, g[id(b2.weight)], g[id(b2.bias)])
+        dy2_4 = dy2.view(n, p_, q_, width)
+        if st == 1:
+            da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, 1, 1).view(-1, width)
+        else:
+            gi = torch.ops.aten.convolution_backward(dy2_4.permute(0, 3, 1, 2), a1.view(n, h, w, width).permute(
+                0, 3, 1, 2), w2, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+            da1 = _rows(gi)
+        L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
+        # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
+        dy1, _, _, _ = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])
+        if blk.down is not None:
+            yd, md, idd = sv[13:16]
+            bd, wd = blk.down.bn, blk.down.conv.weight
+            dyd, _, _, _ = L.bn_bwd(dres, None, yd, bd.weight, md, idd, False, False, g[id(bd.weight)],
+                                    g[id(bd.bias)])
+            if st == 1:
+                dx2 = gemm(dyd, True, _mat(wd), False)
+                gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
+            else:
+                dsub = gemm(dyd, True, _mat(wd), False).view(n, p_, q_, c)
+                dx4 = torch.zeros(n, h, w, c, device=x2.device, dtype=x2.dtype)
+                dx4[:, ::st, ::st, :] = dsub
+                dx2 = dx4.view(-1, c)
+                L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
+                             st, 0)
+        else:
+            dx2 = dres
+        gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
+        gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
+        grads = []
+        for p, (a, direct) in zip(params, accs):
+            if direct:
+                grad_sink.notify(p)
+                grads.append(None)
+            else:
+                grads.append(a.to(p.dtype))
+        return (dx2.view(n, h, w, c).permute(0, 3, 1, 2), None, *grads)
+
+
+def fused_ok(blk, x):
+    ws = [blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight]
+    return (blk.training and x.is_cuda and x.dtype == torch.bfloat16 and all(v.dtype == torch.bfloat16 for v in ws)
+            and x.shape[1] % 64 == 0 and blk.c1.conv.weight.shape[0] % 64 == 0)
+
+
+def bottleneck(blk, x):
+    params = [blk.c1.conv.weight, blk.c1.bn.weight, blk.c1.bn.bias, blk.c2.conv.weight, blk.c2.bn.weight,
+              blk.c2.bn.bias, blk.c3.conv.weight, blk.c3.bn.weight, blk.c3.bn.bias]
+    if blk.down is not None:
+        params += [blk.down.conv.weight, blk.down.bn.weight, blk.down.bn.bias]
+    return _BottleneckFn.apply(x, blk, *params)

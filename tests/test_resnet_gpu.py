@@ -30,6 +30,48 @@ def test_resnet_tiny_loss_decreases():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
+@pytest.mark.parametrize("cin,width,stride", [(64, 64, 1), (256, 64, 1), (256, 128, 2), (512, 128, 1)])
+@pytest.mark.parametrize("flat", [False, True])
+def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat):
+    """The hand-written bottleneck backward equals the layer-by-layer autograd path."""
+    from dtg.models.resnet import Bottleneck
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    blocks = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        b = Bottleneck(cin, width, stride).to(dev).to(memory_format=torch.channels_last)
+        for bn in (b.c1.bn, b.c2.bn, b.c3.bn):
+            bn.weight.data.uniform_(0.5, 1.5)  # c3 is zero-initialised: make the branch matter
+        b.fused = fused
+        b.train()
+        if flat:
+            FlatParams(b)
+        else:
+            for p in b.parameters():
+                if p.dim() > 1:
+                    p.data = p.data.to(torch.bfloat16)
+        blocks.append(b)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x0 = torch.randn(4, cin, 14, 14, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = None
+    outs, grads = [], []
+    for b in blocks:
+        x = x0.clone().requires_grad_()
+        y = b(x)
+        if gy is None:
+            gy = torch.randn(y.shape, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y.backward(gy)
+        outs.append(y.float())
+        grads.append([x.grad.float()] + [p.grad.float().clone() for p in b.parameters()])
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    assert rel(outs[1], outs[0]) < 1e-2
+    for ga, gb in zip(grads[1], grads[0]):
+        assert rel(ga, gb) < 3e-2, rel(ga, gb)
+    for ba, bb in zip(blocks[1].buffers(), blocks[0].buffers()):
+        assert torch.allclose(ba, bb, rtol=1e-3, atol=1e-4)
+
+
 def test_resnet50_step_matches_reference_direction():
     """One ResNet-50 step on a small batch: finite loss, grads flow into the flat buffer."""
     torch.manual_seed(0)
