@@ -6,7 +6,8 @@ images/sec for the whole job, one process per MI355X (RCCL over xGMI).
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
 
 Weak scaling: every GPU trains a fixed per-GPU batch (default 256 images of 224x224, synthetic
-data, random-init weights).  A timed step is the full training step: forward, fused softmax-xent,
+data, random-init weights).  ``--model bert`` measures BASELINE.json config 5 instead (BERT-base
+pre-training, MLM + NSP, seq 128, per-GPU batch 64, fused Adam; sequences/sec).  A timed step is the full training step: forward, fused softmax-xent,
 backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD apply.  W untimed
 warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
 is the MAX over ranks; rank 0 prints one JSON line.
@@ -27,10 +28,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default 256 resnet / 64 bert)")
+    ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket_mb", type=float, default=32.0)
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--model", default="resnet50")
     return ap.parse_known_args(argv)[0]
 
@@ -51,22 +53,47 @@ def main(argv=None):
     if device.type == "cuda":
         ops.lib()  # fail loudly if the HIP kernels are missing
     dtype = torch.bfloat16
-    model = resnet.resnet50().to(device)
-    model = model.to(memory_format=torch.channels_last)
-    flat = FlatParams(model, compute_dtype=dtype)
-    dp = DataParallel(flat, bucket_mb=a.bucket_mb)
-    dp.broadcast_parameters(0)
-    opt = FusedSGD(flat, lr=a.lr * world, momentum=0.9, weight_decay=5e-5)
-    x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
-    model.train()
+    if a.model == "bert":
+        from dtg.models import bert
+        from dtg.optim import FusedAdam
+        a.batch = a.batch or 64
+        cfg = bert.BertConfig.base()
+        model = bert.BertForPreTraining(cfg).to(device)
+        flat = FlatParams(model, compute_dtype=dtype)
+        dp = DataParallel(flat, bucket_mb=a.bucket_mb)
+        dp.broadcast_parameters(0)
+        opt = FusedAdam(flat, lr=a.lr or 1e-4, weight_decay=0.01)
+        batch = bert.synthetic_batch(a.batch, a.seq, cfg, device, max_predictions=20, seed=rank)
+        model.train()
 
-    def step():
-        out = model(x)
-        loss = ops.softmax_cross_entropy(out, y)
-        loss.backward()
-        dp.finish()
-        opt.step(grad_scale=dp.grad_scale)
-        return loss
+        def step():
+            loss = model(*batch)
+            loss.backward()
+            dp.finish()
+            opt.step(grad_scale=dp.grad_scale)
+            return loss
+        metric, unit = "sequences/sec (whole node) BERT-base pre-training sync DP", "sequences/sec"
+        conf = {"model": "BERT-base (MLM+NSP)", "seq_len": a.seq, "optimizer": "adam-wd (fused)"}
+    else:
+        a.batch = a.batch or 256
+        model = resnet.resnet50().to(device)
+        model = model.to(memory_format=torch.channels_last)
+        flat = FlatParams(model, compute_dtype=dtype)
+        dp = DataParallel(flat, bucket_mb=a.bucket_mb)
+        dp.broadcast_parameters(0)
+        opt = FusedSGD(flat, lr=(a.lr or 0.1) * world, momentum=0.9, weight_decay=5e-5)
+        x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
+        model.train()
+
+        def step():
+            out = model(x)
+            loss = ops.softmax_cross_entropy(out, y)
+            loss.backward()
+            dp.finish()
+            opt.step(grad_scale=dp.grad_scale)
+            return loss
+        metric, unit = METRIC, "images/sec"
+        conf = {"model": "ResNet-50", "seq_len": None, "image_size": a.image, "optimizer": "momentum-sgd (fused)"}
 
     for _ in range(a.warmup):
         loss = step()
@@ -86,13 +113,13 @@ def main(argv=None):
     gb = a.batch * world
     ips = gb * a.steps / dt
     if rank == 0:
+        config = {"model": conf["model"], "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": conf["seq_len"]}
+        config.update({k: v for k, v in conf.items() if k not in config})
+        config.update({"parallelism": f"dp{world}", "allreduce": f"rccl bf16, {a.bucket_mb:g} MB buckets, overlapped"})
         print(json.dumps({
-            "metric": METRIC, "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+            "metric": metric, "value": round(ips, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"model": "ResNet-50", "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": None,
-                       "image_size": a.image, "parallelism": f"dp{world}", "optimizer": "momentum-sgd (fused)",
-                       "allreduce": f"rccl bf16, {a.bucket_mb:g} MB buckets, overlapped"},
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic", "config": config,
             "final_loss": final_loss}), flush=True)
     comm.shutdown()
 

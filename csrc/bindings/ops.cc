@@ -253,7 +253,7 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor> softmax_xent(Tensor logits, Te
 // out[M,N] = act(alpha * op(A) op(B) + beta*out + bias).  a_kc: A stored [M,K] (else [K,M]);
 // b_kc: B stored [N,K] (else [K,N]).  Row strides are taken from the 2-D tensors.
 void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, double beta,
-          c10::optional<Tensor> bias, int64_t act, int64_t split_k) {
+          c10::optional<Tensor> bias, int64_t act, int64_t split_k, c10::optional<Tensor> aux, int64_t aux_mode) {
   CHECK_CUDA(A);
   CHECK_CUDA(B);
   CHECK_CUDA(out);
@@ -280,6 +280,15 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
     TORCH_CHECK(bias->numel() == N, "bias size mismatch");
     bptr = bias->data_ptr<float>();
   }
+  void* auxp = nullptr;
+  if (aux_mode != 0) {
+    TORCH_CHECK(aux_mode == 1 || aux_mode == 2, "aux_mode in {0, 1, 2}");
+    TORCH_CHECK(aux.has_value() && aux->defined(), "aux_mode needs an aux tensor");
+    TORCH_CHECK(aux->is_cuda() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2, "aux must be bf16 2-D");
+    TORCH_CHECK(aux->size(0) == M && aux->size(1) == N && aux->stride(0) == out.stride(0) && aux->stride(1) == 1,
+                "aux must match out's shape and row stride");
+    auxp = aux->data_ptr();
+  }
   c10::DeviceGuard dg(A.device());
   int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K);
   Tensor ws;
@@ -290,7 +299,7 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
   }
   dtg::gemm_bf16(cbfp(A), A.stride(0), a_kc, cbfp(B), B.stride(0), b_kc, out.data_ptr(), out.stride(0),
                  out.scalar_type() == at::kBFloat16, M, N, K, (float)alpha, (float)beta, bptr, (int)act, sk, wsp,
-                 cur_stream());
+                 cur_stream(), dtg::GemmBatch(), auxp, (int)aux_mode);
 }
 
 // ---- implicit-GEMM convolution -----------------------------------------------------------------
@@ -359,6 +368,8 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
 
 }  // namespace
 
+void register_transformer_ops(pybind11::module_& m);  // transformer_ops.cc
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_supported", &conv_supported);
   m.def("conv_fwd", &conv_fwd);
@@ -377,5 +388,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("relu"), pybind11::arg("want_dres"),
         pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("softmax_xent", &softmax_xent);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"), pybind11::arg("b_kc"),
+        pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
+        pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,
+        pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0);
+  register_transformer_ops(m);
 }

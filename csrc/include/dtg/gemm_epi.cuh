@@ -12,6 +12,8 @@ struct Epi {
   float alpha, beta;
   const float* bias;  // per column (N), may be null
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
+  void* aux = nullptr;  // bf16 [M, ldc] side buffer (see aux_mode)
+  int aux_mode = 0;     // 0 none; 1 store the pre-activation to aux; 2 multiply by act'(aux) (act backward)
 };
 
 __device__ __forceinline__ float apply_act(float v, int act) {
@@ -21,6 +23,17 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     return 0.5f * v * (1.f + tanhf(u));
   }
   return v;
+}
+
+// d act(x) / dx
+__device__ __forceinline__ float act_grad(float x, int act) {
+  if (act == 1) return x > 0.f ? 1.f : 0.f;
+  if (act == 2) {
+    const float k = 0.7978845608028654f;
+    const float t = tanhf(k * (x + 0.044715f * x * x * x));
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+  }
+  return 1.f;
 }
 
 // finish 8 consecutive columns [n, n+8) of row m (n < N; the tail is masked element-wise)
@@ -42,7 +55,23 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
   for (int k = 0; k < 8; ++k) {
     float x = v[k] * e.alpha + e.beta * old[k];
     if (e.bias && k < cnt) x += e.bias[n + k];
-    v[k] = apply_act(x, e.act);
+    v[k] = x;
+  }
+  if (e.aux_mode == 1) {
+    if (vec) store8_bf16((bf16_t*)e.aux + off, v);
+    else
+      for (int k = 0; k < cnt; ++k) ((bf16_t*)e.aux)[off + k] = f2bf(v[k]);
+  }
+  if (e.aux_mode == 2) {
+    float pre[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (vec) load8_bf16((const bf16_t*)e.aux + off, pre);
+    else
+      for (int k = 0; k < cnt; ++k) pre[k] = bf2f(((const bf16_t*)e.aux)[off + k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= act_grad(pre[k], e.act);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = apply_act(v[k], e.act);
   }
   if (vec) {
     if (e.c_bf16) store8_bf16((bf16_t*)e.C + off, v);

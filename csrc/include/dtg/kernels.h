@@ -40,11 +40,41 @@ void softmax_xent(const void* x, int x_bf16, const long long* label, long long B
                   void* dx, float* lse, hipStream_t st);
 
 // ---- GEMM (gemm.hip) -------------------------------------------------------------------------
+// Two-level batch (e.g. [batch, heads] of attention): problem z = zb * nh + zh uses
+// A + zb*sa_b + zh*sa_h etc. (element strides).  count = 1 for a plain GEMM.
+struct GemmBatch {
+  int count = 1, nh = 1;
+  long long sa_b = 0, sa_h = 0, sb_b = 0, sb_h = 0, sc_b = 0, sc_h = 0;
+};
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
 int gemm_pick_split(int M, int N, int K);
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
-               int split_k, float* ws, hipStream_t st);
+               int split_k, float* ws, hipStream_t st, const GemmBatch& batch = GemmBatch(), void* aux = nullptr,
+               int aux_mode = 0);
+
+// ---- transformer blocks (transformer.hip) ------------------------------------------------------
+int ln_max_hidden();
+int ln_bwd_blocks(int T);  // ln_bwd workspace = ln_bwd_blocks(T) * 2H floats
+void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
+            float* mean, float* rstd, int T, int H, float eps, float p_in, uint32_t seed_in, float p_out,
+            uint32_t seed_out, hipStream_t st);
+void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* ws, int T, int H, float p_in,
+            uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st);
+int attn_max_keys();
+void attn_softmax_fwd(const float* sc, const float* mask, bf16_t* P, bf16_t* Pd, int rows, int rows_per_b, int Sk,
+                      float p, uint32_t seed, hipStream_t st);
+void attn_softmax_bwd(const bf16_t* P, const bf16_t* Pd, const float* dPd, bf16_t* dS, int rows, int Sk, float scale,
+                      hipStream_t st);
+int colsum_splits(int T, int N);  // workspace = splits * nsel * N floats
+void colsum(const bf16_t* x, long long ld, int T, int N, const long long* sel, int nsel, void* out, int out_bf16,
+            int accumulate, float* ws, int splits, hipStream_t st);
+void emb_fwd(const long long* ids, const long long* tt, const bf16_t* word, const bf16_t* pos, const bf16_t* type,
+             bf16_t* s, int T, int S, int H, hipStream_t st);
+void emb_word_bwd(const bf16_t* ds, const long long* sorted, const long long* perm, bf16_t* gW, int T, int H,
+                  hipStream_t st);
+void emb_pos_bwd(const bf16_t* ds, bf16_t* gP, int T, int S, int H, hipStream_t st);
 
 // ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
 // which: 0 fwd, 1 dgrad, 2 wgrad

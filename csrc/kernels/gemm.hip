@@ -17,9 +17,17 @@ using namespace gemm;
 
 template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
-                                                     int k_per_split, Epi e, float* __restrict__ ws) {
+                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
+  if (bt.count > 1) {  // batched problem z: offset the operands (element strides)
+    const int zb = blockIdx.z / bt.nh, zh = blockIdx.z % bt.nh;
+    sa.p += zb * bt.sa_b + zh * bt.sa_h;
+    sb.p += zb * bt.sb_b + zh * bt.sb_h;
+    const long long co = zb * bt.sc_b + zh * bt.sc_h;
+    e.C = (char*)e.C + co * (e.c_bf16 ? 2 : 4);
+    if (e.aux) e.aux = (char*)e.aux + co * 2;
+  }
   const int ntiles = gridDim.x;  // tiles per split
   const int t = xcd_remap(blockIdx.x, ntiles);
   const int tm = t / tiles_n, tn = t % tiles_n;
@@ -121,39 +129,41 @@ int gemm_pick_split(int M, int N, int K) {
 
 template <class CF, bool AK, bool BK_, bool GUARD>
 static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
-                   int kps, const Epi& e, float* ws, hipStream_t st) {
+                   int kps, const Epi& e, float* ws, hipStream_t st, const GemmBatch& bt) {
   using SA = std::conditional_t<AK, DenseKC<GUARD>, DenseMC<GUARD>>;
   using SB = std::conditional_t<BK_, DenseKC<GUARD>, DenseMC<GUARD>>;
   SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  dim3 grid(tiles_m * tiles_n, split_k);
+  dim3 grid(tiles_m * tiles_n, split_k, bt.count);
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(NT), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws);
+                     kps, e, ws, bt);
 }
 
 template <class CF, bool GUARD>
 static void launch_layout(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
-                          int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st) {
-  if (a_kc && b_kc) launch<CF, true, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else if (a_kc) launch<CF, true, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else if (b_kc) launch<CF, false, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else launch<CF, false, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+                          int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
+                          const GemmBatch& bt) {
+  if (a_kc && b_kc) launch<CF, true, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else if (a_kc) launch<CF, true, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else if (b_kc) launch<CF, false, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else launch<CF, false, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
 }
 
 template <int BM_, int BN_>
 static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
-                       int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st) {
+                       int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
+                       const GemmBatch& bt) {
   // full tiles -> no bounds checks in the address computation
   const bool full = (M % BM_ == 0) && (N % BN_ == 0) && (K % BK == 0);
   // short K per block -> single-stage ring (half the LDS, 2x the resident workgroups)
   const bool short_k = kps <= 2 * BK;
   if (full) {
-    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-    else launch_layout<Cfg<BM_, BN_, 2>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    else launch_layout<Cfg<BM_, BN_, 2>, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else {
-    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-    else launch_layout<Cfg<BM_, BN_, 2>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+    if (short_k) launch_layout<Cfg<BM_, BN_, 1>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    else launch_layout<Cfg<BM_, BN_, 2>, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   }
 }
 
@@ -169,17 +179,18 @@ void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e
 
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
-               int split_k, float* ws, hipStream_t st) {
+               int split_k, float* ws, hipStream_t st, const GemmBatch& bt, void* aux, int aux_mode) {
   if (M <= 0 || N <= 0) return;
+  if (bt.count > 1) split_k = 1;  // batched problems are small tiles: no split-K
   if (split_k < 1) split_k = 1;
   int kps = (K + split_k - 1) / split_k;
   kps = (kps + BK - 1) / BK * BK;
   if (kps < BK) kps = BK;
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
-  Epi e{C, ldc, c_bf16, alpha, beta, bias, act};
-  if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
-  else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st);
+  Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
+  if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 

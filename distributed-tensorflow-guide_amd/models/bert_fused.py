@@ -1,0 +1,204 @@
+"""BERT building blocks as single autograd nodes with hand-written backward passes (GPU, bf16).
+
+Per encoder layer (T = batch*seq rows, H hidden, I intermediate; all GEMMs on the MFMA kernel):
+
+  forward   qkv = x Wqkv^T + b                      (bias in the GEMM epilogue)
+            ctx = attention(qkv)                     (2 strided-batched GEMMs + softmax/dropout kernel)
+            x1  = LN(x + drop(ctx Wo^T + b))         (LN kernel fuses residual add + dropout)
+            f1  = gelu(x1 W1^T + b1)                 (GELU in the epilogue; pre-activation saved by
+                                                      the same epilogue for backward)
+            out = LN(x1 + drop(f1 W2^T + b2))
+  backward  LN kernels emit both the residual-path gradient and the dropout-masked branch gradient
+            (masks regenerated from the counter hash); dgrad GEMMs accumulate the residual gradient
+            (beta = 1) instead of a separate add; GELU' is applied in the dgrad GEMM epilogue from the
+            saved pre-activation; bias gradients are column-sum kernels into the fp32 flat grads;
+            weight gradients accumulate straight into the flat gradient buffer (grad_sink).
+
+The word embedding is tied to the MLM decoder: the MLM head adds its decoder gradient into the
+embedding's flat gradient without notifying; the embedding node (which runs last in backward)
+adds the lookup gradient and notifies once, so the all-reduce bucket holding the embedding sees
+exactly one "ready" event per step.
+"""
+import torch
+
+from ..ops._native import lib
+from ..ops.gemm import gemm, gelu_bwd
+from ..ops import transformer as T
+from ..parallel import grad_sink
+
+
+def _gacc(p):
+    if grad_sink.enabled(p):
+        return p.grad, True
+    return torch.zeros_like(p, dtype=torch.float32 if p.dim() <= 1 else p.dtype), False
+
+
+def _finish(params, accs, skip_notify=()):
+    grads = []
+    for p, (a, direct) in zip(params, accs):
+        if direct:
+            if not any(p is q for q in skip_notify):
+                grad_sink.notify(p)
+            grads.append(None)
+        else:
+            grads.append(a.to(p.dtype))
+    return grads
+
+
+class _LayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mask_add, geom, holder, *params):
+        L = lib()
+        B, S, nh, eps, p_h, p_a, s_a, s_1, s_2 = geom
+        w_qkv, b_qkv, w_o, b_o, g1, be1, w_1, b_1, w_2, b_2, g2, be2 = params
+        qkv = gemm(x, True, w_qkv, True, bias=b_qkv)
+        cx, P, Pd = T.attention_fwd(qkv, mask_add, B, S, nh, p_a, s_a)
+        ao = gemm(cx, True, w_o, True, bias=b_o)
+        x1, s1, m1, r1 = L.ln_fwd(ao, x, g1, be1, eps, p_h, s_1, 0.0, 0, True)
+        pre = torch.empty(x.shape[0], w_1.shape[0], device=x.device, dtype=x.dtype)
+        f1 = torch.empty_like(pre)
+        L.gemm(x1, True, w_1, True, f1, 1.0, 0.0, b_1, 2, 0, pre, 1)
+        f2 = gemm(f1, True, w_2, True, bias=b_2)
+        out, s2, m2, r2 = L.ln_fwd(f2, x1, g2, be2, eps, p_h, s_2, 0.0, 0, True)
+        ctx.geom = geom
+        ctx.mod_params = holder.params  # parameter objects: their .grad is the flat-buffer view
+        ctx.save_for_backward(x, qkv, P, Pd, cx, x1, s1, m1, r1, pre, f1, s2, m2, r2, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        L = lib()
+        B, S, nh, eps, p_h, p_a, s_a, s_1, s_2 = ctx.geom
+        sv = ctx.saved_tensors
+        x, qkv, P, Pd, cx, x1, s1, m1, r1, pre, f1, s2, m2, r2 = sv[:14]
+        w_qkv, b_qkv, w_o, b_o, g1, be1, w_1, b_1, w_2, b_2, g2, be2 = sv[14:]
+        mod_params = ctx.mod_params
+        accs = [_gacc(p) for p in mod_params]
+        (gw_qkv, _), (gb_qkv, _), (gw_o, _), (gb_o, _), (gg1, _), (gbe1, _), (gw_1, _), (gb_1, _), (gw_2, _), \
+            (gb_2, _), (gg2, _), (gbe2, _) = accs
+        H = x.shape[1]
+        dout = dout.contiguous()
+        # LN2: ds2 -> x1 (residual path), df2 -> f2 (dropout branch)
+        ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True)
+        L.colsum(df2, gb_2, True)
+        gemm(df2, False, f1, False, out=gw_2, beta=1.0)                       # dW2 += df2^T f1
+        dpre = torch.empty_like(pre)
+        L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 2)      # df1 * gelu'(pre)
+        L.colsum(dpre, gb_1, True)
+        gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                      # dW1 += dpre^T x1
+        if p_h <= 0:  # df2 aliases ds2: it has been consumed above; accumulate the residual grad into a copy
+            ds2 = ds2.clone()
+        gemm(dpre, True, w_1, False, out=ds2, beta=1.0)                       # dx1 = dpre W1 + ds2
+        # LN1: ds1 -> x (residual), dao -> attention output projection
+        ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True)
+        L.colsum(dao, gb_o, True)
+        gemm(dao, False, cx, False, out=gw_o, beta=1.0)
+        dcx = gemm(dao, True, w_o, False)
+        dqkv = torch.empty_like(qkv)
+        T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
+        L.colsum(dqkv, gb_qkv, True)
+        gemm(dqkv, False, x, False, out=gw_qkv, beta=1.0)
+        if p_h <= 0:
+            ds1 = ds1.clone()
+        gemm(dqkv, True, w_qkv, False, out=ds1, beta=1.0)                     # dx = dqkv Wqkv + ds1
+        grads = _finish(mod_params, accs)
+        return (ds1, None, None, None, *grads)
+
+
+class _Holder:
+    """Carries the module's parameter objects into ctx (autograd only sees their tensors)."""
+    __slots__ = ("params",)
+
+    def __init__(self, params):
+        self.params = params
+
+
+def encoder_layer(layer, x, mask_add, B, S, cfg, p_h, p_a, s_a, s_1, s_2):
+    params = layer.params()
+    geom = (B, S, cfg.heads, cfg.eps, p_h, p_a, s_a, s_1, s_2)
+    return _LayerFn.apply(x, mask_add, geom, _Holder(params), *params)
+
+
+# ---- embeddings ----------------------------------------------------------------------------------------
+class _EmbFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, tt, geom, holder, word, pos, typ, g, b):
+        L = lib()
+        S, eps, p, seed = geom
+        s = L.emb_fwd(ids, tt, word, pos, typ, S)
+        y, _, mean, rstd = L.ln_fwd(s, None, g, b, eps, 0.0, 0, p, seed, False)
+        ctx.geom = geom
+        ctx.mod_params = holder.params
+        ctx.save_for_backward(ids, tt, s, mean, rstd, g)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = lib()
+        S, eps, p, seed = ctx.geom
+        ids, tt, s, mean, rstd, g = ctx.saved_tensors
+        word, pos, typ, gam, bet = ctx.mod_params
+        accs = [_gacc(q) for q in ctx.mod_params]
+        (gw, _), (gp, _), (gt, _), (gg, _), (gb, _) = accs
+        ds, _ = L.ln_bwd(dy.contiguous(), s, g, mean, rstd, gg, gb, 0.0, 0, p, seed, False)
+        srt, perm = torch.sort(ids)
+        L.emb_word_bwd(ds, srt, perm, gw)
+        L.emb_pos_bwd(ds, gp, S)
+        if tt is not None:
+            L.colsum(ds, gt.view(-1), True, tt, typ.shape[0])
+        else:
+            L.colsum(ds, gt[0], True)
+        grads = _finish(ctx.mod_params, accs)
+        return (None, None, None, None, *grads)
+
+
+def embeddings(model, ids, tt, S, p, seed):
+    e = model.emb
+    cfg = model.cfg
+    params = [e.word, e.pos, e.tok_type, e.ln_g, e.ln_b]
+    ids1 = ids.reshape(-1).contiguous()
+    tt1 = tt.reshape(-1).contiguous() if tt is not None else None
+    return _EmbFn.apply(ids1, tt1, (S, cfg.eps, p, seed), _Holder(params), *params)
+
+
+# ---- masked-LM head (transform + tied decoder + cross-entropy) -------------------------------------------
+class _MLMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hm, labels, geom, holder, w_t, b_t, g, b, word, dec_bias):
+        L = lib()
+        eps, denom = geom
+        pre = torch.empty(hm.shape[0], w_t.shape[0], device=hm.device, dtype=hm.dtype)
+        a = torch.empty_like(pre)
+        L.gemm(hm, True, w_t, True, a, 1.0, 0.0, b_t, 2, 0, pre, 1)
+        t, _, mean, rstd = L.ln_fwd(a, None, g, b, eps, 0.0, 0, 0.0, 0, False)
+        logits = gemm(t, True, word, True, bias=dec_bias)
+        loss_rows, dlogits, _ = L.softmax_xent(logits, labels, 1.0 / denom, True)
+        ctx.mod_params = holder.params
+        ctx.save_for_backward(hm, pre, a, mean, rstd, t, dlogits, w_t, g, word)
+        return loss_rows.sum() / denom
+
+    @staticmethod
+    def backward(ctx, gout):
+        L = lib()
+        hm, pre, a, mean, rstd, t, dlogits, w_t, g, word = ctx.saved_tensors
+        w_t_p, b_t_p, g_p, b_p, word_p, dec_p = ctx.mod_params
+        accs = [_gacc(q) for q in ctx.mod_params]
+        (gwt, _), (gbt, _), (gg, _), (gb, _), (gword, _), (gdec, _) = accs
+        dl = dlogits * gout.to(dlogits.dtype)
+        L.colsum(dl, gdec, True)
+        gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
+        dt = gemm(dl, True, word, False)                               # [P, H]
+        da, _ = L.ln_bwd(dt, a, g, mean, rstd, gg, gb, 0.0, 0, 0.0, 0, False)
+        dpre = gelu_bwd(da, pre)
+        L.colsum(dpre, gbt, True)
+        gemm(dpre, False, hm, False, out=gwt, beta=1.0)
+        dhm = gemm(dpre, True, w_t, False)
+        # the embedding node notifies the shared word-embedding gradient after adding its part
+        grads = _finish(ctx.mod_params, accs, skip_notify=(word_p,))
+        return (dhm, None, None, None, *grads)
+
+
+def mlm_head(model, hm, labels, num_valid):
+    params = [model.mlm_w, model.mlm_b, model.mlm_ln_g, model.mlm_ln_b, model.emb.word, model.mlm_bias]
+    return _MLMFn.apply(hm.contiguous(), labels.contiguous(), (model.cfg.eps, float(num_valid)), _Holder(params),
+                        *params)

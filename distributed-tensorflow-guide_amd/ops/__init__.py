@@ -8,4 +8,5 @@ from .batchnorm import batch_norm_act  # noqa: F401
 from .loss import softmax_cross_entropy  # noqa: F401
 from .gemm import gemm, linear  # noqa: F401
 from .conv import conv2d  # noqa: F401
+from . import transformer  # noqa: F401
 from . import optim_kernels  # noqa: F401

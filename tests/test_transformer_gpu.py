@@ -1,0 +1,208 @@
+"""Transformer kernels (csrc/kernels/transformer.hip, batched/aux GEMM) vs fp32 PyTorch references,
+and the fused BERT vs its plain-PyTorch oracle."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dtg  # noqa: F401
+from dtg.ops import lib, transformer as T
+from dtg.ops.gemm import gelu_bwd
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda")
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_gemm_gelu_aux_store_and_grad():
+    torch.manual_seed(0)
+    M, N, K = 256, 384, 192
+    a = torch.randn(M, K, device=dev).bfloat16()
+    w = torch.randn(N, K, device=dev).bfloat16() * 0.1
+    bias = torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    pre = torch.empty_like(out)
+    lib().gemm(a, True, w, True, out, 1.0, 0.0, bias, 2, 0, pre, 1)
+    ref_pre = a.float() @ w.float().t() + bias
+    assert rel(pre, ref_pre) < 1e-2
+    assert rel(out, F.gelu(ref_pre, approximate="tanh")) < 1e-2
+    # aux_mode 2: out = (dy @ W) * gelu'(pre)
+    dy = torch.randn(M, N, device=dev).bfloat16()
+    w2 = torch.randn(N, N, device=dev).bfloat16() * 0.1
+    d = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    lib().gemm(dy, True, w2, False, d, 1.0, 0.0, None, 2, 0, pre, 2)
+    ref = gelu_bwd((dy.float() @ w2.float()), pre.float())
+    assert rel(d, ref) < 2e-2
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_strided_batched(a_kc, b_kc):
+    torch.manual_seed(1)
+    B, nh, M, N, K = 3, 4, 128, 64, 128
+    # operands packed like attention: [B, rows, nh * cols] with a head offset inside the row
+    A = torch.randn(B, (M if a_kc else K), nh * (K if a_kc else M), device=dev).bfloat16()
+    Bm = torch.randn(B, (N if b_kc else K), nh * (K if b_kc else N), device=dev).bfloat16()
+    C = torch.zeros(B, M, nh * N, device=dev, dtype=torch.float32)
+    lda, ldb, ldc = A.shape[2], Bm.shape[2], C.shape[2]
+    T.gemm_batched(A, a_kc, Bm, b_kc, C, M, N, K, lda, ldb, ldc, B, nh, (A[0].numel(), lda // nh),
+                   (Bm[0].numel(), ldb // nh), (C[0].numel(), N), alpha=0.5)
+    for b in range(B):
+        for h in range(nh):
+            if a_kc:
+                a = A[b][:, h * K:(h + 1) * K].float()
+            else:
+                a = A[b][:, h * M:(h + 1) * M].float().t()
+            if b_kc:
+                bb = Bm[b][:, h * K:(h + 1) * K].float().t()
+            else:
+                bb = Bm[b][:, h * N:(h + 1) * N].float()
+            ref = 0.5 * a @ bb
+            assert rel(C[b][:, h * N:(h + 1) * N], ref) < 1e-2, (b, h)
+
+
+@pytest.mark.parametrize("H", [768, 1024, 64])
+@pytest.mark.parametrize("p_in,p_out", [(0.0, 0.0), (0.1, 0.0), (0.0, 0.1)])
+def test_layernorm_fwd_bwd(H, p_in, p_out):
+    torch.manual_seed(2)
+    Tn = 300
+    h = torch.randn(Tn, H, device=dev).bfloat16()
+    res = torch.randn(Tn, H, device=dev).bfloat16() if p_out == 0 else None
+    g = torch.rand(H, device=dev) + 0.5
+    b = torch.randn(H, device=dev)
+    y, s, mean, rstd = lib().ln_fwd(h, res, g, b, 1e-12, p_in, 11, p_out, 13, True)
+    hr = h.float().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = T.layer_norm_ref(hr, res.float() if res is not None else None, gr, br, 1e-12, p_in, 11, p_out, 13)
+    assert rel(y, yr) < 1e-2
+    dy = torch.randn(Tn, H, device=dev).bfloat16()
+    yr.backward(dy.float())
+    dg = torch.zeros(H, device=dev)
+    db = torch.zeros(H, device=dev)
+    ds, dh = lib().ln_bwd(dy, s, g, mean, rstd, dg, db, p_in, 11, p_out, 13, True)
+    assert rel(dh, hr.grad) < 2e-2
+    assert rel(dg, gr.grad) < 1e-2 and rel(db, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("S", [128, 512, 96])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_softmax(S, p):
+    torch.manual_seed(3)
+    B, nh = 2, 3
+    sc = torch.randn(B * nh * S, S, device=dev) * 3
+    am = torch.ones(B, S, device=dev)
+    am[1, S - 7:] = 0
+    mask = T.mask_additive(am)
+    P, Pd = lib().attn_softmax_fwd(sc, mask, nh * S, p, 77)
+    scr = sc.clone().requires_grad_()
+    pr = torch.softmax(scr.view(B, nh * S, S) + mask.view(B, 1, S), -1).view(-1, S)
+    assert rel(P, pr) < 1e-2
+    pdr = T.dropout_ref(pr, p, 77)
+    assert rel(Pd, pdr) < 1e-2
+    dPd = torch.randn_like(sc)
+    pdr.backward(dPd)
+    dS = lib().attn_softmax_bwd(P, Pd, dPd, 0.5)
+    assert rel(dS, 0.5 * scr.grad) < 2e-2
+
+
+def test_colsum_and_selector():
+    torch.manual_seed(4)
+    x = torch.randn(1000, 776, device=dev).bfloat16()
+    out = torch.ones(776, device=dev)
+    lib().colsum(x, out, True)
+    assert rel(out, 1 + x.float().sum(0)) < 1e-3
+    sel = torch.randint(0, 2, (1000,), device=dev)
+    o2 = torch.zeros(2, 776, device=dev, dtype=torch.bfloat16)
+    lib().colsum(x, o2.view(-1), False, sel, 2)
+    ref = torch.stack([x.float()[sel == v].sum(0) for v in range(2)])
+    assert rel(o2, ref) < 1e-2
+    # strided rows (a column slice of a wider matrix)
+    wide = torch.randn(64, 2304, device=dev).bfloat16()
+    o3 = torch.zeros(768, device=dev)
+    lib().colsum(wide[:, 768:1536], o3, True)
+    assert rel(o3, wide[:, 768:1536].float().sum(0)) < 1e-3
+
+
+def test_embedding_fwd_bwd():
+    torch.manual_seed(5)
+    V, P, H, B, S = 1000, 64, 256, 4, 32
+    word = torch.randn(V, H, device=dev).bfloat16()
+    pos = torch.randn(P, H, device=dev).bfloat16()
+    typ = torch.randn(2, H, device=dev).bfloat16()
+    ids = torch.randint(0, 50, (B * S,), device=dev)  # many repeats -> long sorted runs
+    tt = torch.randint(0, 2, (B * S,), device=dev)
+    s = lib().emb_fwd(ids, tt, word, pos, typ, S)
+    posid = torch.arange(B * S, device=dev) % S
+    ref = word.float()[ids] + pos.float()[posid] + typ.float()[tt]
+    assert rel(s, ref) < 1e-2
+    ds = torch.randn(B * S, H, device=dev).bfloat16()
+    gW = torch.zeros(V, H, device=dev, dtype=torch.bfloat16)
+    srt, perm = torch.sort(ids)
+    lib().emb_word_bwd(ds, srt, perm, gW)
+    refW = torch.zeros(V, H, device=dev).index_add_(0, ids, ds.float())
+    assert rel(gW, refW) < 1e-2
+    gP = torch.zeros(P, H, device=dev, dtype=torch.bfloat16)
+    lib().emb_pos_bwd(ds, gP, S)
+    refP = torch.zeros(P, H, device=dev).index_add_(0, posid, ds.float())
+    assert rel(gP, refP) < 1e-2
+
+
+def _bert_pair(cfg, seed=0):
+    from dtg.models.bert import BertForPreTraining
+    torch.manual_seed(seed)
+    fused = BertForPreTraining(cfg).to(dev)
+    for p in fused.parameters():
+        if p.dim() == 2:
+            p.data = p.data.bfloat16()
+    ref = BertForPreTraining(cfg).to(dev)
+    ref.load_state_dict({k: v.float() for k, v in fused.state_dict().items()})
+    ref.fused = False
+    return fused, ref
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_bert_fused_matches_reference(dropout):
+    from dtg.models.bert import BertConfig, synthetic_batch
+    cfg = BertConfig(vocab_size=1024, hidden=128, layers=2, heads=2, intermediate=512, max_position=128,
+                     dropout=dropout, attn_dropout=dropout)
+    fused, ref = _bert_pair(cfg)
+    batch = synthetic_batch(4, 64, cfg, dev, max_predictions=8, seed=3)
+    am = batch[2].clone()
+    am[1, 50:] = 0
+    batch = batch[:2] + (am,) + batch[3:]
+    lf = fused(*batch)
+    lr = ref(*batch)
+    assert abs(lf.item() - lr.item()) < 2e-2 * abs(lr.item()), (lf.item(), lr.item())
+    lf.backward()
+    lr.backward()
+    worst = []
+    for (n, pf), pr in zip(fused.named_parameters(), ref.parameters()):
+        r = rel(pf.grad, pr.grad)
+        worst.append((r, n))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 5e-2, worst[:5]
+
+
+def test_bert_flat_adam_trains():
+    from dtg.models.bert import BertConfig, BertForPreTraining, synthetic_batch
+    from dtg.parallel import FlatParams, DataParallel
+    from dtg.optim import FusedAdam
+    torch.manual_seed(0)
+    cfg = BertConfig(vocab_size=1024, hidden=128, layers=2, heads=2, intermediate=512, max_position=128)
+    model = BertForPreTraining(cfg).to(dev)
+    flat = FlatParams(model)
+    dp = DataParallel(flat)
+    opt = FusedAdam(flat, lr=1e-3, weight_decay=0.01)
+    batch = synthetic_batch(8, 64, cfg, dev, max_predictions=8, seed=1)
+    losses = []
+    for _ in range(40):
+        loss = model(*batch)
+        loss.backward()
+        dp.finish()
+        opt.step(dp.grad_scale)
+        losses.append(loss.item())
+    assert all(math.isfinite(v) for v in losses)
+    assert losses[-1] < 0.5 * losses[0], losses

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: tests, benchmark, profile.  Every GPU step has its own time limit; a
 # crash/fault/timeout (exit >= 124 or signal) stops the session so nothing else touches the GPU.
-# Usage: tools/gpu_session.sh [steps...]   steps: test bench bench_miopen prof smoke
+# Usage: tools/gpu_session.sh [steps...]   steps: test test_tf bench bench_bert bench_miopen prof prof_bert kbench smoke
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -25,6 +25,10 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     test) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    test_tf) run pytest_tf 600 python -m pytest tests/test_transformer_gpu.py -m gpu -q ;;
+    bench_bert) run bench_bert 600 python bench.py --model bert --steps 20 --warmup 5 ;;
+    prof_bert) run prof_bert 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bert -o run --output-format csv -- \
+            python3 bench.py --model bert --steps 5 --warmup 3 ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
