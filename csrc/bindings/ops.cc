@@ -369,6 +369,7 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
 }  // namespace
 
 void register_transformer_ops(pybind11::module_& m);  // transformer_ops.cc
+void register_pool_ops(pybind11::module_& m);         // pool_ops.cc
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_supported", &conv_supported);
@@ -393,4 +394,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,
         pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0);
   register_transformer_ops(m);
+  register_pool_ops(m);
 }

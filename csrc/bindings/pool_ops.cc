@@ -1,0 +1,76 @@
+// PyTorch bindings for NHWC pooling (pool.hip); registered into dtg._C by ops.cc.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "dtg/kernels.h"
+
+namespace {
+
+using at::Tensor;
+using dtg::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+const bf16_t* cbfp(const Tensor& t) { return reinterpret_cast<const bf16_t*>(t.data_ptr()); }
+bf16_t* bfp(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+
+void check_nhwc8(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, what, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(), what, " must be a contiguous [N,H,W,C] tensor");
+  TORCH_CHECK(t.size(3) % 8 == 0, what, ": C % 8 == 0 required");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() % 16) == 0, what, " must be 16-byte aligned");
+}
+
+// x: [N,H,W,C] -> (y [N,P,Q,C], argmax-in-window uint8 [N,P,Q,C])
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  check_nhwc8(x, "x");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && pad >= 0 && pad < k, "unsupported pooling window");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty output");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, P, Q, C}, x.options());
+  auto idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  dtg::maxpool_fwd(cbfp(x), bfp(y), idx.data_ptr<uint8_t>(), N, H, W, C, k, s, pad, P, Q, cur_stream());
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  check_nhwc8(dy, "dy");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dy.sizes() && idx.is_contiguous(),
+              "idx must be uint8 shaped like dy");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK((H + 2 * pad - k) / s + 1 == P && (W + 2 * pad - k) / s + 1 == Q, "pool geometry mismatch");
+  c10::DeviceGuard dg(dy.device());
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dtg::maxpool_bwd(cbfp(dy), idx.data_ptr<uint8_t>(), bfp(dx), N, (int)H, (int)W, C, k, s, pad, P, Q, cur_stream());
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x) {
+  check_nhwc8(x, "x");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, C}, x.options());
+  dtg::avgpool_fwd(cbfp(x), bfp(y), N, HW, C, cur_stream());
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.is_contiguous(), "dy [N,C]");
+  TORCH_CHECK(dy.size(1) % 8 == 0, "C % 8 == 0 required");
+  const int N = dy.size(0), C = dy.size(1);
+  c10::DeviceGuard dg(dy.device());
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  dtg::avgpool_bwd(cbfp(dy), bfp(dx), N, (int)(H * W), C, cur_stream());
+  return dx;
+}
+
+}  // namespace
+
+void register_pool_ops(pybind11::module_& m) {
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+}

@@ -55,12 +55,11 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 
 // ---- transformer blocks (transformer.hip) ------------------------------------------------------
 int ln_max_hidden();
-int ln_bwd_blocks(int T);  // ln_bwd workspace = ln_bwd_blocks(T) * 2H floats
 void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
             float* mean, float* rstd, int T, int H, float eps, float p_in, uint32_t seed_in, float p_out,
             uint32_t seed_out, hipStream_t st);
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* ws, int T, int H, float p_in,
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, int T, int H, float p_in,
             uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st);
 int attn_max_keys();
 void attn_softmax_fwd(const float* sc, const float* mask, bf16_t* P, bf16_t* Pd, int rows, int rows_per_b, int Sk,
@@ -75,6 +74,14 @@ void emb_fwd(const long long* ids, const long long* tt, const bf16_t* word, cons
 void emb_word_bwd(const bf16_t* ds, const long long* sorted, const long long* perm, bf16_t* gW, int T, int H,
                   hipStream_t st);
 void emb_pos_bwd(const bf16_t* ds, bf16_t* gP, int T, int S, int H, hipStream_t st);
+
+// ---- pooling, NHWC (pool.hip) -----------------------------------------------------------------
+void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad, int P,
+                 int Q, hipStream_t st);
+void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int k, int s, int pad,
+                 int P, int Q, hipStream_t st);
+void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
 
 // ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
 // which: 0 fwd, 1 dgrad, 2 wgrad

@@ -17,7 +17,8 @@ using namespace gemm;
 
 template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
-                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt) {
+                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
+                                                     int* __restrict__ counters) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   if (bt.count > 1) {  // batched problem z: offset the operands (element strides)
@@ -50,6 +51,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N,
       else
         for (int k = 0; k < 8 && n + k < N; ++k) p[k] = v[k];
     });
+    if (counters) splitk_fixup<CF::BM, CF::BN, NT>(ws, split_k, M, N, bm0, bn0, counters + blockIdx.x, e);
     return;
   }
   epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
@@ -136,8 +138,10 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   dim3 grid(tiles_m * tiles_n, split_k, bt.count);
+  int* counters = split_k > 1 ? splitk_counters(tiles_m * tiles_n) : nullptr;
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(NT), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws, bt);
+                     kps, e, ws, bt, counters);
+  if (split_k > 1 && !counters) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 
 template <class CF, bool GUARD>
@@ -191,7 +195,25 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
+}
+
+// Ticket counters for the split-K fixup: one zeroed int per output tile, per device, allocated on
+// first use (outside any graph capture) and kept zero by the kernels themselves.
+int* splitk_counters(int n_tiles) {
+  constexpr int kMaxDev = 64, kCount = 1 << 16;
+  static int* ptrs[kMaxDev] = {nullptr};
+  if (n_tiles > kCount) return nullptr;  // caller falls back to... never: tiles are bounded by the grid
+  int dev = 0;
+  DTG_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDev) return nullptr;
+  if (!ptrs[dev]) {
+    int* p = nullptr;
+    DTG_HIP_CHECK(hipMalloc(&p, kCount * sizeof(int)));
+    DTG_HIP_CHECK(hipMemset(p, 0, kCount * sizeof(int)));
+    DTG_HIP_CHECK(hipDeviceSynchronize());
+    ptrs[dev] = p;
+  }
+  return ptrs[dev];
 }
 
 }  // namespace dtg

@@ -1,9 +1,10 @@
 // Transformer (BERT) building blocks on gfx950, bf16 activations, fp32 statistics:
 //   * LayerNorm fwd with fused residual add + dropout of the branch input (and optional dropout
 //     of the output, BERT's embedding LayerNorm), bwd with the dropout masks regenerated from a
-//     counter hash (no mask tensors) and deterministic two-pass gamma/beta reduction;
+//     counter hash (no mask tensors) and gamma/beta grads accumulated with per-block fp32 atomics;
 //   * attention softmax fwd (additive key mask, attention-probability dropout) and bwd;
-//   * column sums (bias gradients, token-type embedding gradient with a row selector);
+//   * column sums (bias gradients: per-block atomics into the fp32 grad; token-type embedding
+//     gradient with a row selector: two-pass into bf16);
 //   * embedding gather-sum fwd and the deterministic embedding bwd (sorted token segments: one
 //     writer per vocabulary row, no atomics).
 // One wave64 per row everywhere: a lane owns 8-element (16-byte) chunks lane, lane+64, ... so a
@@ -112,12 +113,14 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 // ---- LayerNorm backward ----------------------------------------------------------------------------
 // g = dropout_out'(dy); ds = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat))
 // ds_out = ds (the residual-branch gradient); dh_out = dropout_in'(ds) (the branch gradient);
-// per-block partial sums of g*xhat and g go to ws[block][2H] (reduced by ln_param_reduce).
+// per-block sums of g*xhat and g are added to dgamma/dbeta with fp32 atomics (one per column
+// per block; the grid is capped so the contention per address stays small).
 template <int NCH>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds_out,
-                                                     bf16_t* __restrict__ dh_out, float* __restrict__ ws, int T, int H,
+                                                     bf16_t* __restrict__ dh_out, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, int T, int H,
                                                      uint32_t th_in, float sc_in, uint32_t seed_in, uint32_t th_out,
                                                      float sc_out, uint32_t seed_out) {
   extern __shared__ float red[];  // [4][2H]
@@ -188,25 +191,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kRowsPerBlock; ++w) t += red[w * 2 * H + i];
-    ws[(long long)blockIdx.x * 2 * H + i] = t;
-  }
-}
-
-// dgamma[i] += sum_b ws[b][i]; dbeta[i] += sum_b ws[b][H + i]
-__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int H,
-                                                              float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;
-  float t = 0.f;
-  if (col < 2 * H)
-    for (int b = part; b < nb; b += 4) t += ws[(long long)b * 2 * H + col];
-  red[part][threadIdx.x & 63] = t;
-  __syncthreads();
-  if (part == 0 && col < 2 * H) {
-    t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (col < H) dgamma[col] += t;
-    else dbeta[col - H] += t;
+    atomicAdd(i < H ? dgamma + i : dbeta + (i - H), t);
   }
 }
 
@@ -286,10 +271,11 @@ __global__ void __launch_bounds__(256) attn_softmax_bwd_kernel(const bf16_t* __r
 // ---- column sums (bias grads; token-type grads with a row selector) ------------------------------------
 // Block: 32 column chunks (8 columns each) x 8 row lanes; grid (ceil(N/256), splits).
 // ws[split][v][N] = sum over the split's rows t with sel[t] == v (sel null: v = 0 for all rows).
+// atomic_out: add straight into the fp32 output (accumulate) instead of writing ws partials.
 template <int NS>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __restrict__ x, long long ld, int T,
                                                              int N, const long long* __restrict__ sel,
-                                                             float* __restrict__ ws) {
+                                                             float* __restrict__ ws, float* __restrict__ atomic_out) {
   __shared__ float red[8][NS][256 + 4];
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -323,7 +309,8 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __res
       float t = 0.f;
 #pragma unroll
       for (int r = 0; r < 8; ++r) t += red[r][v][col];
-      ws[((long long)blockIdx.y * NS + v) * N + n] = t;
+      if (atomic_out) atomicAdd(atomic_out + (long long)v * N + n, t);
+      else ws[((long long)blockIdx.y * NS + v) * N + n] = t;
     }
   }
 }
@@ -442,11 +429,11 @@ void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float*
 
 int ln_bwd_blocks(int T) {
   const int b = (T + kRowsPerBlock - 1) / kRowsPerBlock;
-  return b < 1024 ? (b < 1 ? 1 : b) : 1024;
+  return b < 512 ? (b < 1 ? 1 : b) : 512;
 }
 
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* ws, int T, int H, float p_in,
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, int T, int H, float p_in,
             uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st) {
   if (T <= 0) return;
   const uint32_t ti = drop_thresh(p_in), to = drop_thresh(p_out);
@@ -455,13 +442,12 @@ void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* 
   const int nch = (H / 8 + 63) / 64;
   const size_t lds = (size_t)kRowsPerBlock * 2 * H * sizeof(float);
 #define DTG_LNB(NC)                                                                                                  \
-  hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out, ws, \
-                     T, H, ti, si, seed_in, to, so, seed_out)
+  hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
+                     dgamma, dbeta, T, H, ti, si, seed_in, to, so, seed_out)
   if (nch <= 1) DTG_LNB(1);
   else if (nch == 2) DTG_LNB(2);
   else DTG_LNB(4);
 #undef DTG_LNB
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((2 * H + 63) / 64), dim3(256), 0, st, ws, nb, H, dgamma, dbeta);
 }
 
 int attn_max_keys() { return 64 * 16; }
@@ -500,7 +486,7 @@ void attn_softmax_bwd(const bf16_t* P, const bf16_t* Pd, const float* dPd, bf16_
 
 int colsum_splits(int T, int N) {
   const int cb = (N + 255) / 256;
-  int s = (512 + cb - 1) / cb;
+  int s = (256 + cb - 1) / cb;
   const int maxs = (T + 7) / 8;
   if (s > maxs) s = maxs;
   if (s > 256) s = 256;
@@ -511,8 +497,10 @@ void colsum(const bf16_t* x, long long ld, int T, int N, const long long* sel, i
             int accumulate, float* ws, int splits, hipStream_t st) {
   if (T <= 0 || N <= 0) return;
   dim3 grid((N + 255) / 256, splits);
-  if (nsel <= 1) hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws);
-  else hipLaunchKernelGGL(colsum_partial_kernel<2>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws);
+  float* aout = (!out_bf16 && accumulate) ? (float*)out : nullptr;
+  if (nsel <= 1) hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout);
+  else hipLaunchKernelGGL(colsum_partial_kernel<2>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout);
+  if (aout) return;
   const int nsn = (nsel <= 1 ? 1 : 2) * N;
   hipLaunchKernelGGL(colsum_reduce_kernel, dim3((nsn + 255) / 256), dim3(256), 0, st, ws, splits, nsn, out, out_bf16,
                      accumulate);

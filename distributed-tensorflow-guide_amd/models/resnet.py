@@ -7,9 +7,9 @@ residual add (one HIP kernel pass instead of three).
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import resnet_fused
+from ..ops.pool import max_pool2d, global_avg_pool
 from .layers import ConvBN, Linear
 
 
@@ -51,9 +51,9 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         x = self.stem(x)
-        x = F.max_pool2d(x, 3, 2, 1)
+        x = max_pool2d(x, 3, 2, 1)
         x = self.blocks(x)
-        x = x.mean(dim=(2, 3))
+        x = global_avg_pool(x)
         return self.fc(x)
 
 

@@ -9,4 +9,5 @@ from .loss import softmax_cross_entropy  # noqa: F401
 from .gemm import gemm, linear  # noqa: F401
 from .conv import conv2d  # noqa: F401
 from . import transformer  # noqa: F401
+from .pool import max_pool2d, global_avg_pool  # noqa: F401
 from . import optim_kernels  # noqa: F401

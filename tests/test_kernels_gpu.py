@@ -193,3 +193,32 @@ def test_axpby():
     ref = 0.5 * a + 2.0 * g.float()
     K.axpby(a, g, 0.5, 2.0)
     assert torch.allclose(a, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape,k,s,pad", [((4, 64, 112, 112), 3, 2, 1), ((8, 32, 28, 28), 2, 2, 0),
+                                           ((2, 16, 15, 13), 3, 2, 1)])
+def test_maxpool_fwd_bwd(shape, k, s, pad):
+    from dtg.ops.pool import max_pool2d
+    torch.manual_seed(0)
+    x = torch.randn(shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xr = x.float().requires_grad_()
+    xd = x.clone().requires_grad_()
+    y = max_pool2d(xd, k, s, pad)
+    yr = torch.nn.functional.max_pool2d(xr, k, s, pad)
+    assert torch.equal(y.float(), yr)
+    dy = torch.randn(yr.shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert torch.allclose(xd.grad.float(), xr.grad, atol=1e-2, rtol=1e-2)
+
+
+def test_global_avg_pool():
+    from dtg.ops.pool import global_avg_pool
+    torch.manual_seed(0)
+    x = torch.randn(8, 2048, 7, 7, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xd = x.clone().requires_grad_()
+    y = global_avg_pool(xd)
+    assert torch.allclose(y.float(), x.float().mean(dim=(2, 3)), atol=1e-2)
+    dy = torch.randn(8, 2048, device="cuda").bfloat16()
+    y.backward(dy)
+    assert torch.allclose(xd.grad.float(), (dy.float() / 49)[:, :, None, None].expand(8, 2048, 7, 7), atol=1e-3)
