@@ -84,51 +84,6 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
   }
 }
 
-// Split-K fixup ("last block reduces"; no second launch): call after the block has stored its fp32
-// partial tile into its slab of ws [split_k][M][N].  A per-tile ticket counter (self-resetting, so a
-// zeroed counter array stays zeroed between launches) elects the last of the tile's split_k blocks,
-// which sums all slabs of the tile -- still hot in L2/MALL -- and runs the epilogue.  The agent-scope
-// fences make the slabs of blocks on other XCDs (separate L2s) visible.
-template <int BM, int BN, int NTH>
-__device__ __forceinline__ void splitk_fixup(const float* __restrict__ ws, int split_k, int M, int N, int bm0, int bn0,
-                                             int* counter, const Epi& e) {
-  __shared__ int s_last;
-  __threadfence();  // release this block's slab
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = atomicAdd(counter, 1);
-    s_last = (old == split_k - 1);
-    if (s_last) atomicExch(counter, 0);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();  // acquire the other blocks' slabs
-  const long long plane = (long long)M * N;
-  const bool vec = (N & 3) == 0;
-  constexpr int CPR = BN / 8;
-  for (int idx = threadIdx.x; idx < BM * CPR; idx += NTH) {
-    const int m = bm0 + idx / CPR, n = bn0 + (idx % CPR) * 8;
-    if (m >= M || n >= N) continue;
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const float* p = ws + (long long)m * N + n;
-    if (vec && n + 8 <= N) {
-      for (int k = 0; k < split_k; ++k) {
-        float v[8];
-        load8_f32(p + k * plane, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] += v[j];
-      }
-    } else {
-      for (int k = 0; k < split_k; ++k)
-        for (int j = 0; j < 8 && n + j < N; ++j) s[j] += p[k * plane + j];
-    }
-    epi_store8(e, N, m, n, s);
-  }
-}
-
-// zero-initialised per-device ticket counters for splitk_fixup (allocated once; gemm.hip)
-int* splitk_counters(int n_tiles);
-
 // split-K reduction of fp32 slabs [split][M][N] + the epilogue (gemm.hip)
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st);
 

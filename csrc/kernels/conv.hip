@@ -223,8 +223,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
 template <class CF>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ x, float* __restrict__ ws,
-                                                           int tiles_n, int k_per_split, Epi e,
-                                                           int* __restrict__ counters) {
+                                                           int tiles_n, int k_per_split) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -246,7 +245,6 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   epilogue_staged<CF>(smem, acc, bm0, bn0, Mo, No, [&](int m, int n, float (&v)[8]) {
     store8_f32(slab + (long long)m * No + n, v);
   });
-  if (counters) splitk_fixup<CF::BM, CF::BN, NT>(ws, gridDim.y, Mo, No, bm0, bn0, counters + blockIdx.x, e);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -310,9 +308,8 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
   const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
   dim3 grid(tm * tn, split);
   Epi e{dw, No, dw_bf16, 1.f, beta, nullptr, 0};
-  int* counters = splitk_counters(tm * tn);
-  conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps, e, counters);
-  if (!counters) gemm_splitk_reduce(ws, split, K, No, e, st);
+  conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
+  gemm_splitk_reduce(ws, split, K, No, e, st);
 }
 
 }  // namespace dtg

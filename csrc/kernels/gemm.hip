@@ -17,8 +17,7 @@ using namespace gemm;
 
 template <class CF, bool AKC, bool BKC, class SA, class SB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
-                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
-                                                     int* __restrict__ counters) {
+                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   if (bt.count > 1) {  // batched problem z: offset the operands (element strides)
@@ -51,15 +50,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N,
       else
         for (int k = 0; k < 8 && n + k < N; ++k) p[k] = v[k];
     });
-    if (counters) splitk_fixup<CF::BM, CF::BN, NT>(ws, split_k, M, N, bm0, bn0, counters + blockIdx.x, e);
     return;
   }
   epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
 }
 
+// Split-K reduction: a thread owns 8 consecutive outputs and sums their split_k partials; the
+// split loop is unrolled by 4 so 4 x 32 B of loads are in flight per thread (the reduce is a pure
+// stream: split_k * M * N * 4 bytes in, the epilogue's bytes out).
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int split_k, int M, int N,
                                                             Epi e) {
-  // 8 consecutive columns per thread
   const int cgs = (N + 7) / 8;
   const long long total = (long long)M * cgs;
   const long long plane = (long long)M * N;
@@ -69,22 +69,34 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
     const int m = (int)(i / cgs), n = (int)(i % cgs) * 8;
     const long long off = (long long)m * N + n;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < split_k; ++k) {
-      if (vec) {
+    if (vec) {
+      int k = 0;
+      for (; k + 4 <= split_k; k += 4) {
+        float v0[8], v1[8], v2[8], v3[8];
+        load8_f32(ws + (k + 0) * plane + off, v0);
+        load8_f32(ws + (k + 1) * plane + off, v1);
+        load8_f32(ws + (k + 2) * plane + off, v2);
+        load8_f32(ws + (k + 3) * plane + off, v3);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += (v0[j] + v1[j]) + (v2[j] + v3[j]);
+      }
+      for (; k < split_k; ++k) {
         float v[8];
         load8_f32(ws + k * plane + off, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) s[j] += v[j];
-      } else {
-        for (int j = 0; j < 8 && n + j < N; ++j) s[j] += ws[k * plane + off + j];
       }
+    } else {
+      for (int k = 0; k < split_k; ++k)
+        for (int j = 0; j < 8 && n + j < N; ++j) s[j] += ws[k * plane + off + j];
     }
     epi_store8(e, N, m, n, s);
   }
 }
 
-// Parallel split-K reduction: a block owns 256 consecutive outputs (32 lanes x 8 floats) and its
-// 8 lane-groups stride over the splits; partial sums meet in LDS.  Needs (M*N) % 8 == 0, N % 8 == 0.
+// Large split counts (conv wgrad over N*H*W can split 64-256 ways): a block owns 256 consecutive
+// outputs (32 lanes x 8 floats) and its 8 lane-groups stride over the splits; partial sums meet in
+// LDS.  Needs (M*N) % 8 == 0, N % 8 == 0.
 __global__ void __launch_bounds__(256) splitk_reduce_par_kernel(const float* __restrict__ ws, int split_k, int M,
                                                                 int N, Epi e) {
   __shared__ float red[8][256 + 8];
@@ -138,10 +150,9 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   dim3 grid(tiles_m * tiles_n, split_k, bt.count);
-  int* counters = split_k > 1 ? splitk_counters(tiles_m * tiles_n) : nullptr;
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(NT), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws, bt, counters);
-  if (split_k > 1 && !counters) gemm_splitk_reduce(ws, split_k, M, N, e, st);
+                     kps, e, ws, bt);
+  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 
 template <class CF, bool GUARD>
@@ -172,12 +183,12 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
 }
 
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
-  if (N % 8 == 0) {
+  if (N % 8 == 0 && split_k > 16) {
     const long long plane = (long long)M * N;
     splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e);
   } else {
     const long long total = (long long)M * ((N + 7) / 8);
-    splitk_reduce_kernel<<<grid_for(total, 256, 4096), 256, 0, st>>>(ws, split_k, M, N, e);
+    splitk_reduce_kernel<<<grid_for(total, 256, 1 << 16), 256, 0, st>>>(ws, split_k, M, N, e);
   }
 }
 
@@ -195,25 +206,6 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-}
-
-// Ticket counters for the split-K fixup: one zeroed int per output tile, per device, allocated on
-// first use (outside any graph capture) and kept zero by the kernels themselves.
-int* splitk_counters(int n_tiles) {
-  constexpr int kMaxDev = 64, kCount = 1 << 16;
-  static int* ptrs[kMaxDev] = {nullptr};
-  if (n_tiles > kCount) return nullptr;  // caller falls back to... never: tiles are bounded by the grid
-  int dev = 0;
-  DTG_HIP_CHECK(hipGetDevice(&dev));
-  if (dev < 0 || dev >= kMaxDev) return nullptr;
-  if (!ptrs[dev]) {
-    int* p = nullptr;
-    DTG_HIP_CHECK(hipMalloc(&p, kCount * sizeof(int)));
-    DTG_HIP_CHECK(hipMemset(p, 0, kCount * sizeof(int)));
-    DTG_HIP_CHECK(hipDeviceSynchronize());
-    ptrs[dev] = p;
-  }
-  return ptrs[dev];
 }
 
 }  // namespace dtg

@@ -1,0 +1,200 @@
+"""Asynchronous parameter server on GPUs: one PS rank keeps the parameters in HBM, workers push
+gradients and pull parameters with point-to-point RCCL send/recv (``torch.distributed`` "nccl"
+backend = RCCL over xGMI; "gloo" on the CPU for tests).
+
+This is the GPU-scale form of the reference's between-graph async training (SURVEY §2.3 Hogwild,
+DOWNPOUR, ADAG; §2.4 (b); BASELINE.json config 4 "ResNet-50 async parameter-server, 1 PS + 7
+workers intra-node (RCCL send/recv)").  Reference semantics kept:
+
+* Hogwild (``Hogwild/Hogwild.py:44-57``): every worker gradient is applied on the PS as soon as it
+  arrives, no locking across workers; a worker computes on whatever parameters it last pulled.
+* DOWNPOUR / ADAG window (``DOWNPOUR/DOWNPOUR.py:63-102``, ``ADAG/ADAG.py:69-90``): a worker runs
+  ``window`` local steps (optionally applying a local optimizer), accumulates their gradients and
+  pushes the sum (DOWNPOUR) or the mean (ADAG); the PS applies it with the global optimizer.
+
+MI355X design: parameters and optimizer state live in the PS GPU's flat buffers (FlatParams); a
+push is one RCCL send per dtype group (bf16 compute grads + fp32 norm/bias grads), a pull is one
+send of the bf16 compute mirror + fp32 group.  The PS serves all workers concurrently: it keeps
+one receive posted per worker (RCCL runs each PS<->worker pair on its own communicator/stream),
+applies whichever gradient lands first with the fused HIP optimizer kernel, snapshots the updated
+parameters into that worker's send buffer (so later applies cannot tear an in-flight send) and
+sends them back.
+"""
+import time
+
+import torch
+import torch.distributed as dist
+
+_GRAD, _DONE = 1, 2
+
+
+def _group_payload_grads(flat):
+    return [g.grad for g in flat]
+
+
+def _group_payload_params(flat):
+    # what the model reads: the bf16 mirror of the compute group, the fp32 master of the fp32 group
+    return [g.mirror if g.mirror is not None else g.master for g in flat]
+
+
+class AsyncPSWorker:
+    """Worker side.  ``begin()`` pulls the current parameters, ``step_done()`` after every backward
+    pushes/pulls every ``window`` steps, ``finish()`` tells the PS this worker is done (the PS's
+    ``serve()`` returns when all workers finished; a new begin()/serve() round may follow)."""
+
+    def __init__(self, flat, ps_rank=0, window=1, window_mode="sum", local_optimizer=None, group=None):
+        assert window_mode in ("sum", "mean")
+        self.flat = flat
+        self.ps = ps_rank
+        self.pg = group
+        self.window = max(1, int(window))
+        self.window_mode = window_mode
+        self.local_opt = local_optimizer
+        dev = next(iter(flat)).master.device
+        self.dev = dev
+        self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._acc = [torch.zeros_like(g.grad) for g in flat] if (self.window > 1 and local_optimizer) else None
+        self.local_step = 0
+        self.pushes = 0
+
+    def begin(self):
+        """Initial pull (replaces the chief's assign_global + sleep(10) bootstrap,
+        DOWNPOUR/DOWNPOUR.py:129-135)."""
+        self.pull()
+
+    def pull(self):
+        for buf in _group_payload_params(self.flat):
+            dist.recv(buf, src=self.ps, group=self.pg)
+        if self.local_opt is not None:
+            # the local optimizer updates the fp32 master: re-seed it from the pulled parameters
+            for g in self.flat:
+                if g.mirror is not None:
+                    g.master.copy_(g.mirror)
+
+    def step_done(self):
+        """Call once per local step after backward.  Pushes/pulls every ``window`` steps; returns
+        True when an exchange with the PS happened."""
+        self.local_step += 1
+        if self._acc is not None:
+            # DOWNPOUR-style: accumulate this step's gradient, then take a local optimizer step
+            for a, g in zip(self._acc, self.flat):
+                a.add_(g.grad.to(a.dtype))
+            self.local_opt.step()
+        if self.local_step % self.window:
+            return False
+        grads = self._acc if self._acc is not None else _group_payload_grads(self.flat)
+        self._hdr[0] = _GRAD
+        self._hdr[1] = self.local_step
+        dist.send(self._hdr, dst=self.ps, group=self.pg)
+        works = [dist.isend(t, dst=self.ps, group=self.pg) for t in grads]
+        for w in works:
+            w.wait()
+        for t in grads:
+            t.zero_()
+        if self._acc is not None:
+            self.flat.zero_grad()
+        self.pull()
+        self.pushes += 1
+        return True
+
+    def finish(self):
+        self._hdr[0] = _DONE
+        self._hdr[1] = self.local_step
+        dist.send(self._hdr, dst=self.ps, group=self.pg)
+
+
+class AsyncPSServer:
+    """PS side: ``serve()`` runs until every worker sent DONE; returns the number of updates."""
+
+    def __init__(self, flat, optimizer, workers, window=1, window_mode="sum", group=None, staleness_log=False):
+        self.flat = flat
+        self.opt = optimizer
+        self.workers = list(workers)
+        self.pg = group
+        self.gscale = 1.0 / window if window_mode == "mean" else 1.0
+        dev = next(iter(flat)).master.device
+        self.dev = dev
+        self._recv = {w: [torch.empty_like(g.grad) for g in flat] for w in self.workers}
+        self._snap = {w: [torch.empty_like(t) for t in _group_payload_params(flat)] for w in self.workers}
+        self._hdr = {w: torch.zeros(2, dtype=torch.int64, device=dev) for w in self.workers}
+        self._send_works = {w: [] for w in self.workers}
+        self.updates = 0
+        self.version = 0
+        self._pulled_version = {w: 0 for w in self.workers}
+        self.staleness = [] if staleness_log else None
+        self.per_worker = {w: 0 for w in self.workers}
+
+    def _send_params(self, w):
+        for prev in self._send_works[w]:
+            prev.wait()  # the snapshot buffer is about to be overwritten
+        snap = self._snap[w]
+        for s, p in zip(snap, _group_payload_params(self.flat)):
+            s.copy_(p)
+        self._send_works[w] = [dist.isend(s, dst=w, group=self.pg) for s in snap]
+        self._pulled_version[w] = self.version
+
+    def _apply(self, w):
+        bufs = self._recv[w]
+        saved = [g.grad for g in self.flat]
+        try:
+            for g, b in zip(self.flat, bufs):
+                g.grad = b
+            self.opt.step(grad_scale=self.gscale, zero_grad=False)
+        finally:
+            for g, s in zip(self.flat, saved):
+                g.grad = s
+        if self.staleness is not None:
+            self.staleness.append(self.version - self._pulled_version[w])
+        self.version += 1
+        self.updates += 1
+        self.per_worker[w] += 1
+
+    def _handle(self, w):
+        """Header from worker w has landed: DONE -> False; else receive, apply, reply -> True."""
+        if int(self._hdr[w][0].item()) == _DONE:
+            return False
+        for b in self._recv[w]:
+            dist.recv(b, src=w, group=self.pg)
+        self._apply(w)
+        self._send_params(w)
+        return True
+
+    def serve(self, poll_sleep=0.0):
+        for w in self.workers:
+            self._send_params(w)
+        if dist.get_backend(self.pg) == "gloo":
+            self._serve_any_source()
+        else:
+            self._serve_polling(poll_sleep)
+        for w in self.workers:
+            for s in self._send_works[w]:
+                s.wait()
+        return self.updates
+
+    def _serve_polling(self, poll_sleep):
+        # RCCL: one header receive posted per worker (each on its pair communicator); serve
+        # whichever completes first
+        pending = {w: dist.irecv(self._hdr[w], src=w, group=self.pg) for w in self.workers}
+        while pending:
+            progressed = False
+            for w in list(pending):
+                if not pending[w].is_completed():
+                    continue
+                pending[w].wait()
+                progressed = True
+                if self._handle(w):
+                    pending[w] = dist.irecv(self._hdr[w], src=w, group=self.pg)
+                else:
+                    del pending[w]
+            if not progressed and poll_sleep:
+                time.sleep(poll_sleep)
+
+    def _serve_any_source(self):
+        # gloo: receive-from-any-source gives arrival order directly
+        live = set(self.workers)
+        hdr = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        while live:
+            w = dist.recv(hdr, group=self.pg)  # returns the sender's global rank
+            self._hdr[w].copy_(hdr)
+            if not self._handle(w):
+                live.discard(w)

@@ -1,0 +1,153 @@
+"""GPU-style async parameter server (parallel/async_ps.py) exercised with gloo ranks on the CPU.
+
+* 1 PS + 1 worker: asynchronous == sequential, so the PS parameters must equal a local replay;
+* 1 PS + 2 workers (Hogwild): every pushed gradient is applied exactly once, both workers learn;
+* window=3, mean (ADAG-style): the PS applies steps/3 updates of the averaged gradient.
+"""
+import os
+import sys
+
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _model():
+    import dtg  # noqa: F401
+    from dtg.models.layers import Linear
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Linear(8, 16, act="relu")
+            self.b = Linear(16, 3)
+
+        def forward(self, x):
+            return self.b(self.a(x))
+    torch.manual_seed(0)
+    return M()
+
+
+def _data(seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(32, 8, generator=g), torch.randint(0, 3, (32,), generator=g)
+
+
+def _rank(rank, world, port, steps, window, mode, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import dtg  # noqa: F401
+        from dtg import ops
+        from dtg.optim import FusedSGD
+        from dtg.parallel import FlatParams, comm
+        from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
+        comm.init("gloo")
+        model = _model()
+        flat = FlatParams(model, compute_dtype=torch.float32)
+        if rank == 0:
+            opt = FusedSGD(flat, lr=0.1, momentum=0.0)
+            ps = AsyncPSServer(flat, opt, workers=range(1, world), window=window, window_mode=mode,
+                               staleness_log=True)
+            n = ps.serve()
+            q.put((rank, "ok", {"updates": n, "per_worker": dict(ps.per_worker),
+                                "w": [t.clone() for t in (g.master for g in flat)],
+                                "staleness": list(ps.staleness)}))
+        else:
+            w = AsyncPSWorker(flat, ps_rank=0, window=window, window_mode=mode)
+            w.begin()
+            x, y = _data(rank)
+            losses = []
+            for _ in range(steps):
+                loss = ops.softmax_cross_entropy(model(x), y)
+                loss.backward()
+                w.step_done()
+                losses.append(loss.item())
+            w.finish()
+            q.put((rank, "ok", {"losses": losses, "pushes": w.pushes}))
+        comm.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+        raise
+
+
+def _run(world, steps, window=1, mode="sum"):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, steps, window, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, status, payload = q.get(timeout=240)
+        assert status == "ok", status
+        out[r] = payload
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+def _replay(steps, window, mode, seed=1):
+    """Sequential single-worker SGD with the same window rule."""
+    import dtg  # noqa: F401
+    from dtg import ops
+    model = _model()
+    x, y = _data(seed)
+    params = list(model.parameters())
+    acc = [torch.zeros_like(p) for p in params]
+    for i in range(steps):
+        loss = ops.softmax_cross_entropy(model(x), y)
+        grads = torch.autograd.grad(loss, params)
+        for a, g in zip(acc, grads):
+            a.add_(g)
+        if (i + 1) % window == 0:
+            scale = 1.0 / window if mode == "mean" else 1.0
+            with torch.no_grad():
+                for p, a in zip(params, acc):
+                    p.sub_(0.1 * scale * a)
+                    a.zero_()
+    return {n: p.detach() for n, p in model.named_parameters()}
+
+
+def _ps_params_by_name(out):
+    import dtg  # noqa: F401
+    from dtg.parallel import FlatParams
+    model = _model()
+    flat = FlatParams(model, compute_dtype=torch.float32)
+    for g, w in zip(flat, out[0]["w"]):
+        g.master.copy_(w)
+    return dict(flat.named_masters())
+
+
+def test_async_ps_single_worker_equals_sequential():
+    out = _run(2, steps=12)
+    assert out[0]["updates"] == 12 and out[1]["pushes"] == 12
+    assert all(s == 0 for s in out[0]["staleness"])
+    got = _ps_params_by_name(out)
+    ref = _replay(12, 1, "sum")
+    for n, v in ref.items():
+        assert torch.allclose(got[n], v, atol=1e-5), n
+
+
+def test_async_ps_window_mean_equals_sequential():
+    out = _run(2, steps=12, window=3, mode="mean")
+    assert out[0]["updates"] == 4
+    got = _ps_params_by_name(out)
+    ref = _replay(12, 3, "mean")
+    for n, v in ref.items():
+        assert torch.allclose(got[n], v, atol=1e-5), n
+
+
+def test_async_ps_two_workers_hogwild():
+    out = _run(3, steps=30)
+    assert out[0]["updates"] == 60
+    assert out[0]["per_worker"] == {1: 30, 2: 30}
+    for r in (1, 2):
+        ls = out[r]["losses"]
+        assert ls[-1] < ls[0], ls

@@ -46,6 +46,10 @@ def bench_gemm(iters, out):
         cases.append((f"r50 wgrad {hw}x{hw} {cin}->{cout}", cout, cin, M, False, False))
     for (M, N, K) in [(16384, 2304, 768), (16384, 768, 768), (16384, 3072, 768), (16384, 768, 3072), (4096, 4096, 4096)]:
         cases.append((f"gemm {M}x{N}x{K}", M, N, K, True, True))
+    # BERT-base backward at 8192 tokens: dgrad (B = W, MN-contiguous) and wgrad (both MN-contiguous)
+    for (n_out, n_in) in [(2304, 768), (768, 768), (3072, 768), (768, 3072)]:
+        cases.append((f"bert dgrad {n_out}->{n_in}", 8192, n_in, n_out, True, False))
+        cases.append((f"bert wgrad {n_out}x{n_in}", n_out, n_in, 8192, False, False))
     for name, M, N, K, akc, bkc in cases:
         A = torch.randn((M, K) if akc else (K, M), device=dev, dtype=torch.bfloat16)
         B = torch.randn((N, K) if bkc else (K, N), device=dev, dtype=torch.bfloat16)
