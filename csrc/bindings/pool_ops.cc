@@ -1,4 +1,5 @@
-// PyTorch bindings for NHWC pooling (pool.hip); registered into dtg._C by ops.cc.
+// PyTorch bindings for NHWC pooling (pool.hip) and im2col/col2im (im2col.hip); registered into
+// dtg._C by ops.cc.
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -66,6 +67,32 @@ Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// x [N,H,W,C] (any C) -> cols [N*P*Q, Kp] bf16, Kp >= R*S*C, multiple of 8
+Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(), "x NHWC bf16");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(Kp % 8 == 0 && Kp >= R * S * C, "Kp must be >= R*S*C and a multiple of 8");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "bad stride/pad");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty output");
+  c10::DeviceGuard dg(x.device());
+  auto cols = at::empty({(long long)N * P * Q, Kp}, x.options());
+  dtg::im2col(cbfp(x), bfp(cols), N, H, W, C, R, S, stride, pad, Kp, cur_stream());
+  return cols;
+}
+
+Tensor col2im(Tensor dcols, int64_t N, int64_t H, int64_t W, int64_t C, int64_t R, int64_t S, int64_t stride,
+              int64_t pad) {
+  TORCH_CHECK(dcols.is_cuda() && dcols.scalar_type() == at::kBFloat16 && dcols.dim() == 2 && dcols.is_contiguous(),
+              "dcols bf16 2-D");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dcols.size(0) == N * P * Q && dcols.size(1) >= R * S * C && dcols.size(1) % 8 == 0, "dcols shape");
+  c10::DeviceGuard dg(dcols.device());
+  auto dx = at::empty({N, H, W, C}, dcols.options());
+  dtg::col2im(cbfp(dcols), bfp(dx), N, H, W, C, R, S, stride, pad, dcols.size(1), cur_stream());
+  return dx;
+}
+
 }  // namespace
 
 void register_pool_ops(pybind11::module_& m) {
@@ -73,4 +100,6 @@ void register_pool_ops(pybind11::module_& m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("im2col", &im2col);
+  m.def("col2im", &col2im);
 }

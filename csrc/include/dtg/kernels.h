@@ -83,6 +83,12 @@ void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H,
 void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
 void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// ---- im2col / col2im, NHWC (im2col.hip) --------------------------------------------------------
+void im2col(const bf16_t* x, bf16_t* cols, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,
+            hipStream_t st);
+void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,
+            hipStream_t st);
+
 // ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
 // which: 0 fwd, 1 dgrad, 2 wgrad
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);

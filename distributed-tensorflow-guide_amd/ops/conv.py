@@ -5,6 +5,9 @@ Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
         fwd  Y  = X  W^T      dgrad dX = dY W      wgrad dW = dY^T X
   * k x k, C % 64 == 0, K % 64 == 0 -> implicit-GEMM conv (csrc/kernels/conv.hip):
         fwd and wgrad at any stride, dgrad at stride 1 (strided dgrad -> MIOpen)
+  * small channel counts (C % 64 != 0, K % 8 == 0: MNIST's 1/32-channel convs) -> im2col kernel +
+    MFMA GEMM with the bias/ReLU epilogue; dgrad = GEMM + col2im gather kernel
+    (``conv2d_bias_act``)
   * everything else (the 7x7/Cin=3 stem) -> MIOpen through torch
 Weight gradients are accumulated straight into the flat gradient buffer (see parallel/grad_sink).
 """
@@ -99,6 +102,63 @@ class _ConvImplicit(torch.autograd.Function):
         dw4 = torch.empty_like(w4.contiguous())
         lib().conv_wgrad(dy4, x4.contiguous(), dw4, 0.0, st, pad)
         return dx, dw4.permute(0, 3, 1, 2), None, None
+
+
+def _kp(w):
+    return (w.shape[1] * w.shape[2] * w.shape[3] + 7) // 8 * 8
+
+
+def _w_cols(w, kp):
+    """[K, C, R, S] -> [K, Kp] in (r, s, c) column order, zero padded."""
+    k = w.shape[0]
+    w2 = w.permute(0, 2, 3, 1).reshape(k, -1)
+    if w2.shape[1] != kp:
+        w2 = torch.nn.functional.pad(w2, (0, kp - w2.shape[1]))
+    return w2.contiguous()
+
+
+class _ConvIm2col(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, act):
+        n, c, h, wd = x.shape
+        k, _, r, s = w.shape
+        kp = _kp(w)
+        cols = lib().im2col(_nhwc(x).contiguous(), r, s, stride, pad, kp)
+        w2 = _w_cols(w, kp)
+        bias32 = b.float() if b is not None else None
+        y2 = gemm(cols, True, w2, True, bias=bias32, act=act)
+        p_, q_ = (h + 2 * pad - r) // stride + 1, (wd + 2 * pad - s) // stride + 1
+        ctx.save_for_backward(cols, w2, y2 if act == "relu" else None)
+        ctx.geom = (n, c, h, wd, k, r, s, stride, pad, p_, q_, kp)
+        ctx.act = act
+        ctx.has_bias = b is not None
+        ctx.bdtype = b.dtype if b is not None else None
+        ctx.wdtype = w.dtype
+        return y2.view(n, p_, q_, k).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, w2, y2 = ctx.saved_tensors
+        n, c, h, wd, k, r, s, stride, pad, p_, q_, kp = ctx.geom
+        dy2 = _rows(dy)
+        if ctx.act == "relu":
+            dy2 = dy2 * (y2 > 0)
+        dw2 = gemm(dy2, False, cols, False, out_dtype=torch.float32)  # [K, Kp]
+        dw = dw2[:, :r * s * c].reshape(k, r, s, c).permute(0, 3, 1, 2).to(ctx.wdtype)
+        db = dy2.float().sum(0).to(ctx.bdtype) if ctx.has_bias else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcols = gemm(dy2, True, w2, False)  # [NPQ, Kp]
+            dx = lib().col2im(dcols, n, h, wd, c, r, s, stride, pad).permute(0, 3, 1, 2)
+        return dx, dw, db, None, None, None
+
+
+def conv2d_bias_act(x, w, bias=None, stride=1, padding=0, act=None):
+    """act(conv2d(x, w) + bias) for any channel count: im2col + MFMA GEMM (GPU bf16), torch otherwise."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0:
+        return _ConvIm2col.apply(x.contiguous(memory_format=torch.channels_last), w, bias, stride, padding, act)
+    y = F.conv2d(x, w, bias.to(x.dtype) if bias is not None else None, stride, padding)
+    return F.relu(y) if act == "relu" else y
 
 
 def conv2d(x, w, stride=1, padding=0):

@@ -3,3 +3,4 @@ from .flat import FlatParams, FlatGroup  # noqa: F401
 from .ddp import DataParallel  # noqa: F401
 from . import comm  # noqa: F401
 from .async_ps import AsyncPSServer, AsyncPSWorker  # noqa: F401
+from .strategy import MirroredStrategy  # noqa: F401

@@ -222,3 +222,43 @@ def test_global_avg_pool():
     dy = torch.randn(8, 2048, device="cuda").bfloat16()
     y.backward(dy)
     assert torch.allclose(xd.grad.float(), (dy.float() / 49)[:, :, None, None].expand(8, 2048, 7, 7), atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,pad,hw", [(1, 32, 5, 1, 2, 28), (32, 64, 5, 1, 2, 14), (3, 64, 7, 2, 3, 32),
+                                                     (16, 24, 3, 2, 1, 15)])
+def test_conv_im2col_bias_relu(cin, cout, k, stride, pad, hw):
+    from dtg.ops.conv import conv2d_bias_act
+    torch.manual_seed(0)
+    x = torch.randn(4, cin, hw, hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(cout, cin, k, k, device="cuda") * 0.1).bfloat16()
+    b = torch.randn(cout, device="cuda")
+    xd, wd, bd = x.clone().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    xr, wr, br = x.float().requires_grad_(), w.float().requires_grad_(), b.clone().requires_grad_()
+    y = conv2d_bias_act(xd, wd, bd, stride, pad, "relu")
+    yr = F.relu(F.conv2d(xr, wr, br, stride, pad))
+    rel = lambda a, r: ((a.float() - r).norm() / (r.norm() + 1e-12)).item()  # noqa: E731
+    assert rel(y, yr) < 1e-2
+    dy = torch.randn_like(yr)
+    y.backward(dy.bfloat16())
+    yr.backward(dy)
+    assert rel(xd.grad, xr.grad) < 2e-2
+    assert rel(wd.grad, wr.grad) < 2e-2
+    assert rel(bd.grad, br.grad) < 2e-2
+
+
+def test_mnist_cnn_trains_on_gpu():
+    from dtg.models.mnist import MnistCNN, synthetic_mnist
+    from dtg.parallel import MirroredStrategy
+    from dtg.optim import FusedSGD
+    torch.manual_seed(0)
+    s = MirroredStrategy()
+    with s.scope():
+        m = MnistCNN().to(s.device)
+    tr = s.distribute(m, lambda f: FusedSGD(f, lr=0.01, momentum=0.9))
+    for i in range(60):
+        x, y = synthetic_mnist(128, s.device, seed=i)
+        tr.step(lambda: ops.softmax_cross_entropy(m(x), y))
+    x, y = synthetic_mnist(512, s.device, seed=999)
+    with torch.no_grad():
+        acc = (m(x).argmax(1) == y).float().mean().item()
+    assert acc > 0.9, acc
