@@ -44,11 +44,11 @@ typedef __attribute__((address_space(3))) float lds_float;
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-template <int BM_, int BN_, int STAGES_ = 2>
+template <int BM_, int BN_, int STAGES_ = 2, int NW_ = 4>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_;
+  static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_, NW = NW_, NTH = NW_ * 64;
   static constexpr int WM = BM / 64, WN = BN / 64;
-  static_assert(WM * WN == 4, "4 waves of 64x64");
+  static_assert(WM * WN == NW, "one 64x64 sub-tile per wave");
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
@@ -103,10 +103,11 @@ struct DenseMC {
 };
 
 // ---- staging ---------------------------------------------------------------------------------
-// KC tile: ROWS x 64 k (128 B rows); a wave-instruction covers 8 rows
-template <int ROWS, class Src>
+// KC tile: ROWS x 64 k (128 B rows); a wave-instruction covers 8 rows; NW waves share the tile
+template <int ROWS, class Src, int NW = 4>
 __device__ __forceinline__ void stage_kc(const Src& src, lds_char* lds_tile, int row0, int k0, int wave, int lane) {
-  constexpr int PER_WAVE = ROWS / 32;
+  constexpr int PER_WAVE = ROWS / (8 * NW);
+  static_assert(PER_WAVE >= 1, "tile too small for the wave count");
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int r0 = (wave * PER_WAVE + i) * 8;
@@ -119,11 +120,12 @@ __device__ __forceinline__ void stage_kc(const Src& src, lds_char* lds_tile, int
 }
 
 // MC tile: 64 k-rows x ROWS cols (2*ROWS B rows); a wave-instruction covers 512/ROWS k-rows
-template <int ROWS, class Src>
+template <int ROWS, class Src, int NW = 4>
 __device__ __forceinline__ void stage_mc(const Src& src, lds_char* lds_tile, int col0, int k0, int wave, int lane) {
   constexpr int CH = ROWS / 8;          // 16-B chunks per k-row
   constexpr int KPI = 64 / CH;          // k-rows per wave-instruction
-  constexpr int PER_WAVE = 64 / KPI / 4;
+  constexpr int PER_WAVE = 64 / KPI / NW;
+  static_assert(PER_WAVE >= 1, "tile too small for the wave count");
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int kr0 = (wave * PER_WAVE + i) * KPI;
@@ -164,11 +166,15 @@ __device__ __forceinline__ v8bf frag(const lds_char* t, int r0, int ks, int lane
   else return frag_mc<ROWS>(t, r0, ks, lane);
 }
 
-template <bool KC, int ROWS, class Src>
+template <bool KC, int ROWS, class Src, int NW = 4>
 __device__ __forceinline__ void stage(const Src& s, lds_char* t, int rc0, int k0, int wave, int lane) {
-  if constexpr (KC) stage_kc<ROWS>(s, t, rc0, k0, wave, lane);
-  else stage_mc<ROWS>(s, t, rc0, k0, wave, lane);
+  if constexpr (KC) stage_kc<ROWS, Src, NW>(s, t, rc0, k0, wave, lane);
+  else stage_mc<ROWS, Src, NW>(s, t, rc0, k0, wave, lane);
 }
+
+// LDS-DMA instructions one wave issues to stage one K-step of a ROWS-wide operand
+template <int ROWS, int NW>
+constexpr int stage_loads() { return (ROWS * 64 * 2) / (1024 * NW); }
 
 template <class C, bool AKC, bool BKC>
 __device__ __forceinline__ void compute_tile(const lds_char* At, const lds_char* Bt, int wm, int wn, int lane,
@@ -208,6 +214,32 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
       compute_tile<C, AKC, BKC>(smem, smem + C::A_BYTES, wm, wn, lane, acc);
       __syncthreads();
     }
+  } else if constexpr (C::STAGES == 3) {
+    // 3-slot ring, prefetch distance 2, one barrier per K-step.  At the top of step kt the wave's
+    // outstanding LDS-DMA ops are those of tiles kt and kt+1 (LPS each): a counted vmcnt(LPS)
+    // retires tile kt only, the barrier publishes it to all waves (and certifies every wave is done
+    // reading slot (kt+2)%3 = (kt-1)%3), then tile kt+2's DMA is issued and tile kt computed.
+    constexpr int LPS = stage_loads<C::BM, C::NW>() + stage_loads<C::BN, C::NW>();
+    sta(smem, kbeg);
+    stb(smem + C::A_BYTES, kbeg);
+    if (nk > 1) {
+      sta(smem + C::STAGE_BYTES, kbeg + BK);
+      stb(smem + C::STAGE_BYTES + C::A_BYTES, kbeg + BK);
+    }
+    int slot = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 2 < nk) {
+        const int s2 = slot >= 1 ? slot - 1 : 2;  // (kt + 2) % 3
+        sta(smem + s2 * C::STAGE_BYTES, kbeg + (kt + 2) * BK);
+        stb(smem + s2 * C::STAGE_BYTES + C::A_BYTES, kbeg + (kt + 2) * BK);
+      }
+      compute_tile<C, AKC, BKC>(smem + slot * C::STAGE_BYTES, smem + slot * C::STAGE_BYTES + C::A_BYTES, wm, wn, lane,
+                                acc);
+      slot = slot == 2 ? 0 : slot + 1;
+    }
   } else {
     sta(smem, kbeg);
     stb(smem + C::A_BYTES, kbeg);
@@ -231,9 +263,9 @@ __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* s
                                          int kend, f32x4 (&acc)[4][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  mainloop_st<C, AKC, BKC>([&](lds_char* t, int k0) { stage<AKC, C::BM>(sa, t, bm0, k0, wave, lane); },
-                           [&](lds_char* t, int k0) { stage<BKC, C::BN>(sb, t, bn0, k0, wave, lane); }, smem, kbeg,
-                           kend, acc);
+  mainloop_st<C, AKC, BKC>([&](lds_char* t, int k0) { stage<AKC, C::BM, SA, C::NW>(sa, t, bm0, k0, wave, lane); },
+                           [&](lds_char* t, int k0) { stage<BKC, C::BN, SB, C::NW>(sb, t, bn0, k0, wave, lane); },
+                           smem, kbeg, kend, acc);
 }
 
 // ---- fast integer division by a runtime constant (Granlund-Montgomery), n < 2^31 --------------
@@ -287,7 +319,7 @@ __device__ __forceinline__ void epilogue_staged(lds_char* smem, f32x4 (&acc)[4][
     __syncthreads();
     constexpr int CPR = C::BN / 8;  // 8-column groups per row
 #pragma unroll
-    for (int idx = tid; idx < R * CPR; idx += NT) {
+    for (int idx = tid; idx < R * CPR; idx += C::NTH) {
       const int rr = idx / CPR, cg = idx % CPR;
       const int m = bm0 + prow0 + rr, n = bn0 + cg * 8;
       if (m < M && n < N) {

@@ -10,13 +10,14 @@
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
 #include "dtg/gemm_epi.cuh"
+#include <stdlib.h>
 #include <type_traits>
 
 namespace dtg {
 using namespace gemm;
 
 template <class CF, bool AKC, bool BKC, class SA, class SB>
-__global__ void __launch_bounds__(NT, 2) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
+__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
@@ -150,7 +151,7 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   dim3 grid(tiles_m * tiles_n, split_k, bt.count);
-  hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(NT), 0, st, sa, sb, M, N, K, tiles_n, split_k,
+  hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
                      kps, e, ws, bt);
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
@@ -182,6 +183,24 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   }
 }
 
+// 256x128 tile, 8 waves, one workgroup per CU, 3-slot LDS ring with counted vmcnt (prefetch
+// distance 2).  Chosen when the grid still fills the chip with these larger tiles and K per block
+// is long enough for the deeper pipeline to matter.
+static bool use_big(int M, int N, int kps, int split_k, const GemmBatch& bt) {
+  if (const char* f = getenv("DTG_GEMM_BIG")) return f[0] == '1';
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 127) / 128) * split_k * bt.count;
+  return N >= 128 && tiles >= 192 && kps >= 4 * BK;
+}
+
+static void launch_big(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
+                       int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
+                       const GemmBatch& bt) {
+  using CF = Cfg<256, 128, 3, 8>;
+  const bool full = (M % 256 == 0) && (N % 128 == 0) && (K % BK == 0);
+  if (full) launch_layout<CF, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+}
+
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
   if (N % 8 == 0 && split_k > 16) {
     const long long plane = (long long)M * N;
@@ -205,6 +224,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else if (use_big(M, N, kps, split_k, bt)) launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
 }
 

@@ -262,3 +262,19 @@ def test_mnist_cnn_trains_on_gpu():
     with torch.no_grad():
         acc = (m(x).argmax(1) == y).float().mean().item()
     assert acc > 0.9, acc
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (1000, 520, 328), (512, 256, 4096)])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_big_tile_ring(M, N, K, a_kc, b_kc, monkeypatch):
+    """256x128 / 8-wave / 3-slot counted-vmcnt pipeline (forced on) vs fp32 torch."""
+    monkeypatch.setenv("DTG_GEMM_BIG", "1")
+    torch.manual_seed(0)
+    A = torch.randn((M, K) if a_kc else (K, M), device="cuda").bfloat16()
+    B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()
+    bias = torch.randn(N, device="cuda")
+    ref = (A.float() if a_kc else A.float().t()) @ (B.float().t() if b_kc else B.float()) + bias
+    out = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=1)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+    out2 = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=3)
+    assert ((out2 - ref).norm() / ref.norm()).item() < 1e-2

@@ -33,6 +33,8 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
     kbench) run kbench 600 python tools/bench_kernels.py --json gpurun_out/kbench.json ;;
+    kbench_gemm_ab) DTG_GEMM_BIG=0 run kbench_small 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_small.json &&
+                    DTG_GEMM_BIG=1 run kbench_big 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_big.json ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
             python3 bench.py --steps 5 --warmup 3 ;;
     *) run "$s" 900 bash -c "$s" ;;
