@@ -188,6 +188,7 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
 // is long enough for the deeper pipeline to matter.
 static bool use_big(int M, int N, int kps, int split_k, const GemmBatch& bt) {
   if (const char* f = getenv("DTG_GEMM_BIG")) return f[0] == '1';
+  return false;  // measured slower than the 2-block 128x128 ring on every shape (profiles/r01_gemm_ab); opt-in only
   const long long tiles = (long long)((M + 255) / 256) * ((N + 127) / 128) * split_k * bt.count;
   return N >= 128 && tiles >= 192 && kps >= 4 * BK;
 }

@@ -198,3 +198,28 @@ class AsyncPSServer:
             self._hdr[w].copy_(hdr)
             if not self._handle(w):
                 live.discard(w)
+
+
+def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1):
+    """Bootstrap the RCCL/gloo process group from a TF-style ClusterSpec: the PS task 0 is rank 0
+    (its ``host:port`` + ``port_offset`` is the rendezvous), worker i is rank 1 + i.  One process per
+    GPU: pin each process to its GPU with HIP_VISIBLE_DEVICES (see examples/ResNet50/run_async.sh).
+    Returns (rank, world, device)."""
+    import datetime
+    import os
+
+    spec = cluster.as_dict() if hasattr(cluster, "as_dict") else dict(cluster)
+    ps_host, ps_port = spec["ps"][0].rsplit(":", 1)
+    n_workers = len(spec["worker"])
+    rank = 0 if job_name == "ps" else 1 + int(task_index)
+    world = 1 + n_workers
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    device = torch.device("cuda", 0) if backend == "nccl" else torch.device("cpu")
+    if backend == "nccl":
+        torch.cuda.set_device(device)
+    os.environ["MASTER_ADDR"] = "127.0.0.1" if ps_host in ("localhost", "") else ps_host
+    os.environ["MASTER_PORT"] = str(int(ps_port) + port_offset)
+    kw = {"device_id": device} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600), **kw)
+    return rank, world, device

@@ -1,0 +1,77 @@
+"""ResNet-50 with an asynchronous parameter server on GPUs (BASELINE.json config 4: 1 PS + 7
+workers intra-node, RCCL send/recv).  Same launch idiom as the reference's between-graph scripts
+(``--job_name ps|worker --task_index i``, a hard-coded cluster dict; Hogwild/Hogwild.py:20-33),
+but the PS owns a GPU and the parameters live in its HBM (dtg.parallel.async_ps).
+
+    bash run_async.sh [--workers 7] [--steps 50] [--window 1]
+
+--window T > 1 pushes every T local steps: --window_mode sum = DOWNPOUR, mean = ADAG.
+"""
+import argparse
+import time
+
+import _path  # noqa: F401
+
+import torch
+
+import dtg  # noqa: F401
+from dtg import ops
+from dtg.models import resnet
+from dtg.optim import FusedSGD
+from dtg.parallel import FlatParams
+from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker, init_from_cluster
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--job_name", default="")
+    ap.add_argument("--task_index", type=int, default=0)
+    ap.add_argument("--workers", type=int, default=7)
+    ap.add_argument("--base_port", type=int, default=2222)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--window", type=int, default=1)
+    ap.add_argument("--window_mode", default="sum", choices=("sum", "mean"))
+    ap.add_argument("--tiny", action="store_true", help="narrow 4-block ResNet, 32x32 images (CPU smoke tests)")
+    a, _ = ap.parse_known_args()
+    cluster = {"ps": [f"localhost:{a.base_port}"],
+               "worker": [f"localhost:{a.base_port + 1 + i}" for i in range(a.workers)]}
+    rank, world, device = init_from_cluster(cluster, a.job_name, a.task_index)
+    torch.manual_seed(1234)
+    model = (resnet.resnet18_like_tiny(10) if a.tiny else resnet.resnet50()).to(device)
+    model = model.to(memory_format=torch.channels_last)
+    ncls = 10 if a.tiny else 1000
+    flat = FlatParams(model)
+    if a.job_name == "ps":
+        opt = FusedSGD(flat, lr=a.lr, momentum=0.9, weight_decay=5e-5)
+        ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, window_mode=a.window_mode,
+                           staleness_log=True)
+        t0 = time.time()
+        n = ps.serve()
+        dt = time.time() - t0
+        st = ps.staleness
+        print(f"[ps] {n} updates in {dt:.1f}s, per worker {ps.per_worker}, mean staleness "
+              f"{sum(st) / max(1, len(st)):.2f}", flush=True)
+    else:
+        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode)
+        dt_ = torch.bfloat16 if device.type == "cuda" else torch.float32
+        x, y = resnet.synthetic_batch(a.batch, device, dt_, a.image, ncls, seed=rank)
+        w.begin()
+        t0 = time.time()
+        for i in range(a.steps):
+            loss = ops.softmax_cross_entropy(model(x), y)
+            loss.backward()
+            w.step_done()
+            if i % 10 == 0:
+                print(f"[worker {a.task_index}] step {i} loss {loss.item():.4f}", flush=True)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.time() - t0
+        w.finish()
+        print(f"[worker {a.task_index}] {a.steps * a.batch / dt:.1f} images/sec", flush=True)
+
+
+if __name__ == "__main__":
+    main()
