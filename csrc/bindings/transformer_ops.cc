@@ -104,7 +104,7 @@ std::vector<c10::optional<Tensor>> ln_fwd(Tensor h, c10::optional<Tensor> res, T
 // returns (ds, dh): ds = grad wrt s (residual path), dh = grad wrt the dropout input (if want_dh)
 std::vector<c10::optional<Tensor>> ln_bwd(Tensor dy, Tensor s, Tensor gamma, Tensor mean, Tensor rstd,
                                           Tensor dgamma, Tensor dbeta, double p_in, int64_t seed_in, double p_out,
-                                          int64_t seed_out, bool want_dh) {
+                                          int64_t seed_out, bool want_dh, c10::optional<Tensor> dbias) {
   const int64_t H = s.size(-1);
   check_ln(dy, H);
   check_ln(s, H);
@@ -118,12 +118,17 @@ std::vector<c10::optional<Tensor>> ln_bwd(Tensor dy, Tensor s, Tensor gamma, Ten
   const int T = (int)s.size(0);
   TORCH_CHECK(mean.numel() == T && rstd.numel() == T, "stats size mismatch");
   TORCH_CHECK(gamma.numel() == H && dgamma.numel() == H && dbeta.numel() == H, "param size mismatch");
+  if (has(dbias)) {
+    CHECK_F32_CONTIG(*dbias);
+    TORCH_CHECK(dbias->numel() == H, "dbias size mismatch");
+  }
   c10::DeviceGuard dg(s.device());
   auto ds = at::empty_like(s);
   c10::optional<Tensor> dh;
   if (want_dh) dh = p_in > 0 ? at::empty_like(s) : ds;
   dtg::ln_bwd(cbfp(dy), cbfp(s), gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), bfp(ds),
-              (want_dh && p_in > 0) ? bfp(*dh) : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), T, (int)H, (float)p_in, (uint32_t)seed_in, (float)p_out, (uint32_t)seed_out,
+              (want_dh && p_in > 0) ? bfp(*dh) : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+              has(dbias) ? dbias->data_ptr<float>() : nullptr, T, (int)H, (float)p_in, (uint32_t)seed_in, (float)p_out, (uint32_t)seed_out,
               cur_stream());
   return {ds, dh};
 }
@@ -242,7 +247,7 @@ void register_transformer_ops(py::module_& m) {
         py::arg("save_s") = true);
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("dgamma"), py::arg("dbeta"), py::arg("p_in") = 0.0, py::arg("seed_in") = 0, py::arg("p_out") = 0.0,
-        py::arg("seed_out") = 0, py::arg("want_dh") = true);
+        py::arg("seed_out") = 0, py::arg("want_dh") = true, py::arg("dbias") = py::none());
   m.def("attn_softmax_fwd", &attn_softmax_fwd);
   m.def("attn_softmax_bwd", &attn_softmax_bwd);
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = true, py::arg("sel") = py::none(),

@@ -120,17 +120,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds_out,
                                                      bf16_t* __restrict__ dh_out, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, int T, int H,
+                                                     float* __restrict__ dbeta, float* __restrict__ dbias, int T, int H,
                                                      uint32_t th_in, float sc_in, uint32_t seed_in, uint32_t th_out,
                                                      float sc_out, uint32_t seed_out) {
-  extern __shared__ float red[];  // [4][2H]
+  extern __shared__ float red[];  // [4][3H]: gamma, beta, branch-bias partials
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nc = H >> 3;
-  float dg[NCH][8], db[NCH][8];
+  float dg[NCH][8], db[NCH][8], dz[NCH][8];
 #pragma unroll
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dg[j][k] = db[j][k] = 0.f;
+    for (int k = 0; k < 8; ++k) dg[j][k] = db[j][k] = dz[j][k] = 0.f;
   for (int row = blockIdx.x * kRowsPerBlock + wv; row < T; row += gridDim.x * kRowsPerBlock) {
     const long long base = (long long)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
@@ -167,11 +167,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = rstd * (g[j][k] - a - xh[j][k] * b);
         store8_bf16(ds_out + base + c * 8, o);
-        if (dh_out) {
+        if (dh_out || dbias) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k)
+          for (int k = 0; k < 8; ++k) {
             o[k] = (!th_in || keep_elem(seed_in, (uint32_t)(base + c * 8 + k), th_in)) ? o[k] * sc_in : 0.f;
-          store8_bf16(dh_out + base + c * 8, o);
+            dz[j][k] += bf2f(f2bf(o[k]));  // the bias grad of the branch = column sum of the stored dh
+          }
+          if (dh_out) store8_bf16(dh_out + base + c * 8, o);
         }
       }
     }
@@ -182,16 +184,18 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
     if (c < nc)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[wv * 2 * H + c * 8 + k] = dg[j][k];
-        red[wv * 2 * H + H + c * 8 + k] = db[j][k];
+        red[wv * 3 * H + c * 8 + k] = dg[j][k];
+        red[wv * 3 * H + H + c * 8 + k] = db[j][k];
+        red[wv * 3 * H + 2 * H + c * 8 + k] = dz[j][k];
       }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * H; i += blockDim.x) {
+  const int nred = dbias ? 3 * H : 2 * H;
+  for (int i = threadIdx.x; i < nred; i += blockDim.x) {
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < kRowsPerBlock; ++w) t += red[w * 2 * H + i];
-    atomicAdd(i < H ? dgamma + i : dbeta + (i - H), t);
+    for (int w = 0; w < kRowsPerBlock; ++w) t += red[w * 3 * H + i];
+    atomicAdd(i < H ? dgamma + i : (i < 2 * H ? dbeta + (i - H) : dbias + (i - 2 * H)), t);
   }
 }
 
@@ -433,17 +437,17 @@ int ln_bwd_blocks(int T) {
 }
 
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, int T, int H, float p_in,
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* dbias, int T, int H, float p_in,
             uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st) {
   if (T <= 0) return;
   const uint32_t ti = drop_thresh(p_in), to = drop_thresh(p_out);
   const float si = p_in > 0.f ? 1.f / (1.f - p_in) : 1.f, so = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
   const int nb = ln_bwd_blocks(T);
   const int nch = (H / 8 + 63) / 64;
-  const size_t lds = (size_t)kRowsPerBlock * 2 * H * sizeof(float);
+  const size_t lds = (size_t)kRowsPerBlock * 3 * H * sizeof(float);
 #define DTG_LNB(NC)                                                                                                  \
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
-                     dgamma, dbeta, T, H, ti, si, seed_in, to, so, seed_out)
+                     dgamma, dbeta, dbias, T, H, ti, si, seed_in, to, so, seed_out)
   if (nch <= 1) DTG_LNB(1);
   else if (nch == 2) DTG_LNB(2);
   else DTG_LNB(4);

@@ -79,8 +79,7 @@ class _LayerFn(torch.autograd.Function):
         H = x.shape[1]
         dout = dout.contiguous()
         # LN2: ds2 -> x1 (residual path), df2 -> f2 (dropout branch)
-        ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True)
-        L.colsum(df2, gb_2, True)
+        ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True, gb_2)  # + db2 = sum(df2)
         gemm(df2, False, f1, False, out=gw_2, beta=1.0)                       # dW2 += df2^T f1
         dpre = torch.empty_like(pre)
         L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 2)      # df1 * gelu'(pre)
@@ -90,8 +89,7 @@ class _LayerFn(torch.autograd.Function):
             ds2 = ds2.clone()
         gemm(dpre, True, w_1, False, out=ds2, beta=1.0)                       # dx1 = dpre W1 + ds2
         # LN1: ds1 -> x (residual), dao -> attention output projection
-        ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True)
-        L.colsum(dao, gb_o, True)
+        ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True, gb_o)  # + dbo = sum(dao)
         gemm(dao, False, cx, False, out=gw_o, beta=1.0)
         dcx = gemm(dao, True, w_o, False)
         dqkv = torch.empty_like(qkv)

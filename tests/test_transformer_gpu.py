@@ -82,8 +82,10 @@ def test_layernorm_fwd_bwd(H, p_in, p_out):
     yr.backward(dy.float())
     dg = torch.zeros(H, device=dev)
     db = torch.zeros(H, device=dev)
-    ds, dh = lib().ln_bwd(dy, s, g, mean, rstd, dg, db, p_in, 11, p_out, 13, True)
+    dz = torch.zeros(H, device=dev)
+    ds, dh = lib().ln_bwd(dy, s, g, mean, rstd, dg, db, p_in, 11, p_out, 13, True, dz)
     assert rel(dh, hr.grad) < 2e-2
+    assert rel(dz, hr.grad.sum(0)) < 2e-2  # fused branch-bias gradient
     assert rel(dg, gr.grad) < 1e-2 and rel(db, br.grad) < 1e-2
 
 

@@ -37,6 +37,6 @@ for s in $STEPS; do
                     DTG_GEMM_BIG=1 run kbench_big 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_big.json ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
             python3 bench.py --steps 5 --warmup 3 ;;
-    *) run "$s" 900 bash -c "$s" ;;
+    *) run "$(echo "$s" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-80)" 900 bash -c "$s" ;;
   esac
 done
