@@ -236,6 +236,47 @@ void emb_pos_bwd(Tensor ds, Tensor gP, int64_t S) {
   dtg::emb_pos_bwd(cbfp(ds), bfp(gP), T, (int)S, H, cur_stream());
 }
 
+// ---- fused attention (attention.hip) ---------------------------------------------------------------
+// qkv [B*S, 3H] bf16 ([Q | K | V], head h at columns h*64 of each); mask fp32 [B, S] additive or None
+std::vector<Tensor> attn_fused_fwd(Tensor qkv, c10::optional<Tensor> mask, int64_t B, int64_t S, int64_t nh, double p,
+                                   int64_t seed) {
+  CHECK_GPU_BF16_CONTIG(qkv);
+  TORCH_CHECK(dtg::attn_fused_supported((int)S, 64, 0), "fused attention: S % 64 == 0 and S <= 512 required");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * S && qkv.size(1) == 3 * nh * 64, "qkv must be [B*S, 3*nh*64]");
+  TORCH_CHECK(p >= 0 && p < 1, "dropout prob in [0, 1)");
+  if (has(mask)) {
+    CHECK_F32_CONTIG(*mask);
+    TORCH_CHECK(mask->numel() == B * S, "mask must be [B, S]");
+  }
+  c10::DeviceGuard dg(qkv.device());
+  auto out = at::empty({B * S, nh * 64}, qkv.options());
+  auto lse = at::empty({B * nh * S}, qkv.options().dtype(at::kFloat));
+  dtg::attn_fwd(cbfp(qkv), has(mask) ? mask->data_ptr<float>() : nullptr, bfp(out), lse.data_ptr<float>(), (int)B,
+                (int)S, (int)nh, (float)p, (uint32_t)seed, cur_stream());
+  return {out, lse};
+}
+
+Tensor attn_fused_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, c10::optional<Tensor> mask, int64_t B,
+                      int64_t S, int64_t nh, double p, int64_t seed) {
+  CHECK_GPU_BF16_CONTIG(qkv);
+  CHECK_GPU_BF16_CONTIG(out);
+  CHECK_GPU_BF16_CONTIG(dout);
+  CHECK_F32_CONTIG(lse);
+  TORCH_CHECK(dtg::attn_fused_supported((int)S, 64, 1), "fused attention backward: S % 64 == 0 and S <= 128");
+  TORCH_CHECK(qkv.size(0) == B * S && qkv.size(1) == 3 * nh * 64, "qkv shape");
+  TORCH_CHECK(out.sizes() == dout.sizes() && out.size(0) == B * S && out.size(1) == nh * 64, "out/dout shape");
+  TORCH_CHECK(lse.numel() == B * nh * S, "lse size");
+  if (has(mask)) {
+    CHECK_F32_CONTIG(*mask);
+    TORCH_CHECK(mask->numel() == B * S, "mask must be [B, S]");
+  }
+  c10::DeviceGuard dg(qkv.device());
+  auto dqkv = at::empty_like(qkv);
+  dtg::attn_bwd(cbfp(qkv), cbfp(out), cbfp(dout), lse.data_ptr<float>(), has(mask) ? mask->data_ptr<float>() : nullptr,
+                bfp(dqkv), (int)B, (int)S, (int)nh, (float)p, (uint32_t)seed, cur_stream());
+  return dqkv;
+}
+
 }  // namespace
 
 namespace py = pybind11;
@@ -253,6 +294,9 @@ void register_transformer_ops(py::module_& m) {
   m.def("colsum", &colsum, py::arg("x"), py::arg("out"), py::arg("accumulate") = true, py::arg("sel") = py::none(),
         py::arg("nsel") = 1);
   m.def("emb_fwd", &emb_fwd);
+  m.def("attn_fused_fwd", &attn_fused_fwd);
+  m.def("attn_fused_bwd", &attn_fused_bwd);
+  m.def("attn_fused_supported", [](int64_t S, int64_t dh, bool bwd) { return dtg::attn_fused_supported(S, dh, bwd) != 0; });
   m.def("emb_word_bwd", &emb_word_bwd);
   m.def("emb_pos_bwd", &emb_pos_bwd);
 }

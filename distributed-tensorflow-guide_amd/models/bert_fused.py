@@ -19,12 +19,21 @@ embedding's flat gradient without notifying; the embedding node (which runs last
 adds the lookup gradient and notifies once, so the all-reduce bucket holding the embedding sees
 exactly one "ready" event per step.
 """
+import os
+
 import torch
 
 from ..ops._native import lib
 from ..ops.gemm import gemm, gelu_bwd
 from ..ops import transformer as T
 from ..parallel import grad_sink
+
+
+_ATTN = os.environ.get("DTG_ATTN", "fused")  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax)
+
+
+def _fused_attn(S, backward=True):
+    return _ATTN == "fused" and lib().attn_fused_supported(S, 64, backward)
 
 
 def _gacc(p):
@@ -52,7 +61,12 @@ class _LayerFn(torch.autograd.Function):
         B, S, nh, eps, p_h, p_a, s_a, s_1, s_2 = geom
         w_qkv, b_qkv, w_o, b_o, g1, be1, w_1, b_1, w_2, b_2, g2, be2 = params
         qkv = gemm(x, True, w_qkv, True, bias=b_qkv)
-        cx, P, Pd = T.attention_fwd(qkv, mask_add, B, S, nh, p_a, s_a)
+        fused = _fused_attn(S) and w_qkv.shape[0] == 3 * nh * 64
+        if fused:  # flash-style kernel: no [S, S] tensors; P recomputed in backward from the LSE
+            cx, lse = L.attn_fused_fwd(qkv, mask_add, B, S, nh, p_a, s_a)
+            P = Pd = lse
+        else:
+            cx, P, Pd = T.attention_fwd(qkv, mask_add, B, S, nh, p_a, s_a)
         ao = gemm(cx, True, w_o, True, bias=b_o)
         x1, s1, m1, r1 = L.ln_fwd(ao, x, g1, be1, eps, p_h, s_1, 0.0, 0, True)
         pre = torch.empty(x.shape[0], w_1.shape[0], device=x.device, dtype=x.dtype)
@@ -61,6 +75,8 @@ class _LayerFn(torch.autograd.Function):
         f2 = gemm(f1, True, w_2, True, bias=b_2)
         out, s2, m2, r2 = L.ln_fwd(f2, x1, g2, be2, eps, p_h, s_2, 0.0, 0, True)
         ctx.geom = geom
+        ctx.fused_attn = fused
+        ctx.mask_add = mask_add
         ctx.mod_params = holder.params  # parameter objects: their .grad is the flat-buffer view
         ctx.save_for_backward(x, qkv, P, Pd, cx, x1, s1, m1, r1, pre, f1, s2, m2, r2, *params)
         return out
@@ -92,8 +108,11 @@ class _LayerFn(torch.autograd.Function):
         ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True, gb_o)  # + dbo = sum(dao)
         gemm(dao, False, cx, False, out=gw_o, beta=1.0)
         dcx = gemm(dao, True, w_o, False)
-        dqkv = torch.empty_like(qkv)
-        T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
+        if ctx.fused_attn:
+            dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a)
+        else:
+            dqkv = torch.empty_like(qkv)
+            T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
         L.colsum(dqkv, gb_qkv, True)
         gemm(dqkv, False, x, False, out=gw_qkv, beta=1.0)
         if p_h <= 0:

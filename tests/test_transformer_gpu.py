@@ -208,3 +208,56 @@ def test_bert_flat_adam_trains():
         losses.append(loss.item())
     assert all(math.isfinite(v) for v in losses)
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.parametrize("S", [64, 128])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_attention_fwd_bwd(S, p):
+    torch.manual_seed(6)
+    B, nh = 3, 2
+    H = nh * 64
+    qkv = (torch.randn(B * S, 3 * H, device=dev) * 1.5).bfloat16()
+    am = torch.ones(B, S, device=dev)
+    am[1, S - 9:] = 0
+    mask = T.mask_additive(am)
+    out, lse = lib().attn_fused_fwd(qkv, mask, B, S, nh, p, 1234)
+    qr = qkv.float().requires_grad_()
+    ref = T.attention_ref(qr, mask, B, S, nh, p, 1234)
+    assert rel(out, ref) < 1.5e-2
+    # LSE of the scaled+masked scores
+    q, k, _ = qkv.float().view(B, S, 3, nh, 64).permute(2, 0, 3, 1, 4)
+    sc = (q @ k.transpose(-1, -2)) / 8.0 + mask.view(B, 1, 1, S)
+    assert torch.allclose(lse.view(B, nh, S), torch.logsumexp(sc, -1), atol=2e-2)
+    dout = torch.randn(B * S, H, device=dev).bfloat16()
+    ref.backward(dout.float())
+    dqkv = lib().attn_fused_bwd(qkv, out, dout, lse, mask, B, S, nh, p, 1234)
+    for i, name in enumerate("qkv"):
+        a, r = dqkv[:, i * H:(i + 1) * H], qr.grad[:, i * H:(i + 1) * H]
+        assert rel(a, r) < 3e-2, (name, rel(a, r))
+
+
+@pytest.mark.parametrize("S", [256, 512])
+def test_fused_attention_fwd_long(S):
+    torch.manual_seed(7)
+    B, nh = 2, 2
+    H = nh * 64
+    qkv = torch.randn(B * S, 3 * H, device=dev).bfloat16()
+    out, _ = lib().attn_fused_fwd(qkv, None, B, S, nh, 0.0, 0)
+    ref = T.attention_ref(qkv.float(), None, B, S, nh)
+    assert rel(out, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("attn", ["fused", "gemm"])
+def test_bert_attention_paths_agree(attn, monkeypatch):
+    from dtg.models import bert_fused
+    from dtg.models.bert import BertConfig, synthetic_batch
+    monkeypatch.setattr(bert_fused, "_ATTN", attn)
+    cfg = BertConfig(vocab_size=1024, hidden=128, layers=2, heads=2, intermediate=512, max_position=128)
+    fused, ref = _bert_pair(cfg)
+    batch = synthetic_batch(4, 128, cfg, dev, max_predictions=8, seed=5)
+    lf, lr = fused(*batch), ref(*batch)
+    assert abs(lf.item() - lr.item()) < 2e-2 * abs(lr.item())
+    lf.backward()
+    lr.backward()
+    for (n, pf), pr in zip(fused.named_parameters(), ref.parameters()):
+        assert rel(pf.grad, pr.grad) < 5e-2, n
