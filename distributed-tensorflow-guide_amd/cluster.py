@@ -122,7 +122,28 @@ class Server:
         return self._svc
 
     def join(self, timeout=None):
-        """Block until all workers reported done (PS) or shutdown was requested."""
+        """Block until all workers reported done (PS) or shutdown was requested.
+
+        With ``DTG_FAULT=kill_ps_at_step:N`` (tests only, dtg/fault.py) a PS dies abruptly once its
+        ``global_step`` reaches N."""
+        from . import fault
+        kill_at = fault.kill_ps_step() if self.job_name == "ps" else None
+        if kill_at is not None:
+            import os
+            import time
+            t_end = None if timeout is None else time.time() + float(timeout)
+            while t_end is None or time.time() < t_end:
+                if self._svc.join(0.05):
+                    self._svc.stop()
+                    return True
+                try:
+                    gs = int(self._svc.read_var("global_step").reshape(-1)[0])
+                except Exception:  # not created yet
+                    gs = -1
+                if gs >= kill_at:
+                    print("[dtg.fault] killing ps task %d at global_step %d" % (self.task_index, gs), flush=True)
+                    os._exit(fault.KILL_EXIT_CODE)
+            return False
         done = self._svc.join(-1.0 if timeout is None else float(timeout))
         if done:
             self._svc.stop()

@@ -11,6 +11,8 @@ that, when run, applies every gradient where its variable lives:
 """
 from collections import defaultdict
 
+from .. import fault
+
 import numpy as np
 import torch
 
@@ -202,6 +204,9 @@ class _ApplyOp(Op):
             if gs is not None and not gs_done and isinstance(gs, Variable) and gs.remote and gs.ps_task == task:
                 gs_name = gs._name
                 gs_done = True
+            if fault.should_drop_grad():  # DTG_FAULT=drop_grad:P -- the whole push is lost in transit
+                opt.dropped_pushes = getattr(opt, "dropped_pushes", 0) + 1
+                continue
             client = items[0][0]._client()
             step, _ = client.apply(opt.PS_KIND, opt._hyper(lr), bool(opt._use_locking), gs_name,
                                    [(v._name, _as_np(g.float())) for v, g in items], False)

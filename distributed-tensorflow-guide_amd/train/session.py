@@ -19,9 +19,10 @@ import time
 
 import numpy as np
 
+from .. import fault
 from .. import graph as G
 from ..graph import RunContext, to_numpy
-from ..variables import (client_for, global_variables_initializer, local_variables_initializer,
+from ..variables import (client_for, close_connections, global_variables_initializer, local_variables_initializer,
                          report_uninitialized_variables, _this_server)
 from .hooks import (CheckpointSaverHook, SessionRunArgs, SessionRunContext, SessionRunValues, StepCounterHook,
                     StopAtStepHook, SummarySaverHook)
@@ -261,7 +262,46 @@ class _Session:
 
 
 class _MonitoredSession(_Session):
-    pass
+    """A session that survives the loss of a PS task (TF's _RecoverableSession semantics): when a run
+    fails because a PS connection dropped, it reconnects (waiting, with backoff, for the PS to come
+    back), recreates the session -- the chief restores the latest checkpoint into the restarted PS,
+    a non-chief waits until the chief has re-initialised it -- and re-runs the same fetches.
+    SURVEY.md §5.3; exercised by tests/test_fault_cpu.py with DTG_FAULT=kill_ps_at_step:N."""
+
+    max_recoveries = 10
+    _recreate = None
+
+    def run(self, fetches, feed_dict=None, options=None, run_metadata=None):
+        attempts = 0
+        while True:
+            try:
+                return _Session.run(self, fetches, feed_dict, options, run_metadata)
+            except Exception as e:  # noqa: BLE001 - classified below
+                if self._recreate is None or not fault.is_ps_failure(e) or attempts >= self.max_recoveries:
+                    raise
+                attempts += 1
+                print("[dtg] PS failure during run (%s): recovering session (attempt %d)" % (e, attempts),
+                      flush=True)
+                self._recreate()
+
+
+def _make_recreate(sess, sm, scaffold, checkpoint_dir, is_chief, hooks, timeout):
+    def recreate():
+        close_connections()
+        s = _this_server()
+        if s is not None and "ps" in s.cluster.jobs:
+            for t in range(s.cluster.num_tasks("ps")):
+                client_for("ps", t, timeout=timeout).ping()  # blocks (with backoff) until the PS is back
+        if is_chief:
+            sm.prepare_session(sess, scaffold.init_op, scaffold.saver, checkpoint_dir, scaffold.init_fn,
+                               scaffold.init_feed_dict)
+        else:
+            sm.wait_for_session(sess, timeout)
+        print("[dtg] session recovered%s" % (" from " + sess.restored_from if sess.restored_from else ""),
+              flush=True)
+        for h in hooks:
+            h.after_create_session(sess, sess.coord)
+    return recreate
 
 
 def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaffold=None, hooks=None,
@@ -297,6 +337,8 @@ def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaf
         sm.wait_for_session(sess, max_wait_secs)
     for h in all_hooks:
         h.after_create_session(sess, sess.coord)
+    sess._recreate = _make_recreate(sess, sm, scaffold, checkpoint_dir, is_chief, all_hooks,
+                                    float(os.environ.get("DTG_RECOVERY_SECS", "120")))
     atexit.register(sess.close)
     return sess
 

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-STEPS=${*:-"test bench prof"}
+if [ $# -eq 0 ]; then set -- test bench prof; fi
 
 run() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
@@ -22,7 +22,7 @@ run() {  # name timeout cmd...
   return 0
 }
 
-for s in $STEPS; do
+for s in "$@"; do
   case $s in
     test) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
     test_tf) run pytest_tf 600 python -m pytest tests/test_transformer_gpu.py -m gpu -q ;;
@@ -37,6 +37,6 @@ for s in $STEPS; do
                     DTG_GEMM_BIG=1 run kbench_big 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_big.json ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
             python3 bench.py --steps 5 --warmup 3 ;;
-    *) run "$(echo "$s" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-80)" 900 bash -c "$s" ;;
+    *) run "$(echo "$s" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-80)" 900 bash -c "$s < /dev/null" ;;
   esac
 done
