@@ -28,7 +28,7 @@ enum Op : uint16_t {
   APPLY = 5,         // i64 opt, f64 hyper[5], i64 locking, str global_step ("" = none), n, (name, grad)... -> i64 step
   IS_INIT = 6,       // n, names -> n x i64
   LIST = 7,          // -> n, (name, dtype, shape)
-  ACC_CREATE = 8,    // name, i64 dtype, shape tensor template
+  ACC_CREATE = 8,    // name, tensor template (dtype/shape), i64 initial global step
   ACC_APPLY = 9,     // name, i64 local_step, tensor grad -> i64 accepted
   ACC_TAKE = 10,     // name, i64 num_required, f64 timeout_s -> tensor mean
   ACC_SET_STEP = 11, // name, i64 step

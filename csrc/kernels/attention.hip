@@ -22,6 +22,7 @@
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
+#include <stdlib.h>
 
 namespace dtg {
 using namespace gemm;
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
                                                        const bf16_t* __restrict__ dout, const float* __restrict__ lse,
                                                        const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
                                                        int S, int nh, float scale, uint32_t th, float dscale,
-                                                       uint32_t seed) {
+                                                       uint32_t seed, int abl) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
   const int H = nh * 64;
@@ -229,7 +230,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
     }
   }
   // D[q] = sum_d dO[q, d] * O[q, d]  (two threads per row, 32 columns each), LSE, key mask, dQ = 0
-  for (int i = tid; i < 2 * S; i += 256) {
+  for (int i = tid; i < ((abl & 1) ? 0 : 2 * S); i += 256) {
     const int q = i >> 1, half = i & 1;
     float acc = 0.f;
 #pragma unroll
@@ -243,6 +244,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
     acc += __shfl_xor(acc, 1, 64);
     if (half == 0) Ds[q] = acc;
   }
+  if (abl & 1)
+    for (int i = tid; i < S; i += 256) Ds[i] = 0.f;
   for (int i = tid; i < S; i += 256) {
     Ls[i] = lse[(long long)bh * S + i];
     Ms[i] = mask ? mask[(long long)b * S + i] : 0.f;
@@ -272,8 +275,13 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
       f32x4 st[2][2], dpt[2][2];
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        v8bf qb0 = gfrag(Qg, ld, qc + ni * 16, 0, lane), qb1 = gfrag(Qg, ld, qc + ni * 16, 1, lane);
-        v8bf db0 = gfrag(dOg, (long long)H, qc + ni * 16, 0, lane), db1 = gfrag(dOg, (long long)H, qc + ni * 16, 1, lane);
+        v8bf qb0, qb1, db0, db1;
+        if (abl & 8) {
+          qb0 = ka[0][0]; qb1 = ka[0][1]; db0 = va[0][0]; db1 = va[0][1];
+        } else {
+          qb0 = gfrag(Qg, ld, qc + ni * 16, 0, lane); qb1 = gfrag(Qg, ld, qc + ni * 16, 1, lane);
+          db0 = gfrag(dOg, (long long)H, qc + ni * 16, 0, lane); db1 = gfrag(dOg, (long long)H, qc + ni * 16, 1, lane);
+        }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
           f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -329,9 +337,14 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
           dk[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[mi], qbm, dk[mi][j], 0, 0, 0);
           f32x4 dq = f32x4{0.f, 0.f, 0.f, 0.f};
           dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sta[mi], kbm, dq, 0, 0, 0);
+          if (abl & 2) {
+            asm volatile("" ::"v"(dq[0]), "v"(dq[1]), "v"(dq[2]), "v"(dq[3]));
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            __builtin_amdgcn_ds_faddf(dQs + (qc + mi * 16 + rbase + r) * 64 + j * 16 + (lane & 15), dq[r], 0, 0, false);
+            for (int r = 0; r < 4; ++r)
+              __builtin_amdgcn_ds_faddf(dQs + (qc + mi * 16 + rbase + r) * 64 + j * 16 + (lane & 15), dq[r], 0, 0,
+                                        false);
+          }
         }
       }
       lds_fence();  // scratch reuse by the next chunk
@@ -345,8 +358,12 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
         for (int r = 0; r < 4; ++r) {
           const long long row = (long long)b * S + kb + mi * 16 + rbase + r;
           const int col = h * 64 + j * 16 + (lane & 15);
-          dqkv[row * ld + H + col] = f2bf(dk[mi][j][r] * scale);
-          dqkv[row * ld + 2 * H + col] = f2bf(dv[mi][j][r]);
+          if (abl & 4) {
+            asm volatile("" ::"v"(dk[mi][j][r]), "v"(dv[mi][j][r]));
+          } else {
+            dqkv[row * ld + H + col] = f2bf(dk[mi][j][r] * scale);
+            dqkv[row * ld + 2 * H + col] = f2bf(dv[mi][j][r]);
+          }
         }
   }
   __syncthreads();
@@ -390,10 +407,11 @@ void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int
 
 void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, const float* mask,
               bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, hipStream_t st) {
+  static const int abl = getenv("DTG_ATTN_ABL") ? atoi(getenv("DTG_ATTN_ABL")) : 0;  // perf ablation only
   const uint32_t th = drop_th(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * nh), dim3(256), bwd_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                     0.125f, th, ds, seed);
+                     0.125f, th, ds, seed, abl);
 }
 
 }  // namespace dtg
