@@ -43,6 +43,19 @@ static BnGeom bn_geom(long long M, int C) {
   return g;
 }
 
+// The elementwise passes (apply, dx) write no partials, so they run on a much larger grid than the
+// reductions (whose partial count the finalize kernel bounds): ~2048 workgroups.
+static long long elementwise_rpc(const BnGeom& g, long long M) {
+  const int rpp = kBlk / g.tpr;
+  long long nc = 2048 / g.gy;
+  const long long max_chunks = (M + rpp - 1) / rpp;
+  if (nc > max_chunks) nc = max_chunks;
+  if (nc < 1) nc = 1;
+  long long rpc = (M + nc - 1) / nc;
+  rpc = (rpc + rpp - 1) / rpp * rpp;  // whole row groups per chunk
+  return rpc;
+}
+
 long long bn_workspace_floats(long long M, int C) {
   BnGeom g = bn_geom(M, C);
   return (long long)g.nchunk * 2 * C + 4LL * C;
@@ -176,12 +189,7 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
   load8_f32(coef + C + c0, sf);
   const long long m0 = (long long)blockIdx.x * rpc;
   const long long m1 = m0 + rpc < M ? m0 + rpc : M;
-  for (long long m = m0 + ty; m < m1; m += RPP) {
-    const long long off = m * C + c0;
-    float a[8];
-    load8_bf16(x + off, a);
-    float r[8];
-    if constexpr (RES) load8_bf16(res + off, r);
+  auto finish = [&](float (&a)[8], const float (&r)[8], long long off) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = a[k] * sc[k] + sf[k];
@@ -190,6 +198,27 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
       a[k] = v;
     }
     store8_bf16(y + off, a);
+  };
+  long long m = m0 + ty;
+  // 2 rows per iteration: all four 16-B loads are in flight before any math (memory-level parallelism)
+  for (; m + RPP < m1; m += 2 * RPP) {
+    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
+    float a0[8], a1[8], r0[8], r1[8];
+    load8_bf16(x + o0, a0);
+    load8_bf16(x + o1, a1);
+    if constexpr (RES) {
+      load8_bf16(res + o0, r0);
+      load8_bf16(res + o1, r1);
+    }
+    finish(a0, r0, o0);
+    finish(a1, r1, o1);
+  }
+  if (m < m1) {
+    const long long o0 = m * C + c0;
+    float a0[8], r0[8];
+    load8_bf16(x + o0, a0);
+    if constexpr (RES) load8_bf16(res + o0, r0);
+    finish(a0, r0, o0);
   }
 }
 
@@ -212,19 +241,36 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_reduce_kernel(const bf16_t* __res
     load8_f32(sinv + c0, is);
     const long long m0 = (long long)blockIdx.x * rpc;
     const long long m1 = m0 + rpc < M ? m0 + rpc : M;
-    for (long long m = m0 + ty; m < m1; m += RPP) {
-      const long long off = m * C + c0;
-      float g[8], xv[8];
-      load8_bf16(dy + off, g);
-      load8_bf16(x + off, xv);
+    auto acc = [&](float (&g)[8], const float (&xv)[8], const float (&yv)[8]) {
       if constexpr (RELU) {
-        float yv[8];
-        load8_bf16(y + off, yv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] += g[k] * (xv[k] - mu[k]) * is[k]; }
+    };
+    long long m = m0 + ty;
+    for (; m + RPP < m1; m += 2 * RPP) {
+      const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
+      float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
+      load8_bf16(dy + o0, g0);
+      load8_bf16(dy + o1, g1);
+      load8_bf16(x + o0, x0);
+      load8_bf16(x + o1, x1);
+      if constexpr (RELU) {
+        load8_bf16(y + o0, y0);
+        load8_bf16(y + o1, y1);
+      }
+      acc(g0, x0, y0);
+      acc(g1, x1, y1);
+    }
+    if (m < m1) {
+      const long long o0 = m * C + c0;
+      float g0[8], x0[8], y0[8];
+      load8_bf16(dy + o0, g0);
+      load8_bf16(x + o0, x0);
+      if constexpr (RELU) load8_bf16(y + o0, y0);
+      acc(g0, x0, y0);
     }
   }
 #pragma unroll
@@ -258,14 +304,8 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
   load8_f32(coef + 2 * C + c0, cc);
   const long long m0 = (long long)blockIdx.x * rpc;
   const long long m1 = m0 + rpc < M ? m0 + rpc : M;
-  for (long long m = m0 + ty; m < m1; m += RPP) {
-    const long long off = m * C + c0;
-    float g[8], xv[8];
-    load8_bf16(dy + off, g);
-    load8_bf16(x + off, xv);
+  auto finish = [&](float (&g)[8], const float (&xv)[8], const float (&yv)[8], long long off) {
     if constexpr (RELU) {
-      float yv[8];
-      load8_bf16(y + off, yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
     }
@@ -274,6 +314,29 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = a[k] * g[k] + bx[k] * xv[k] + cc[k];
     store8_bf16(dx + off, o);
+  };
+  long long m = m0 + ty;
+  for (; m + RPP < m1; m += 2 * RPP) {  // 2 rows per iteration, up to six 16-B loads in flight
+    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
+    float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
+    load8_bf16(dy + o0, g0);
+    load8_bf16(dy + o1, g1);
+    load8_bf16(x + o0, x0);
+    load8_bf16(x + o1, x1);
+    if constexpr (RELU) {
+      load8_bf16(y + o0, y0);
+      load8_bf16(y + o1, y1);
+    }
+    finish(g0, x0, y0, o0);
+    finish(g1, x1, y1, o1);
+  }
+  if (m < m1) {
+    const long long o0 = m * C + c0;
+    float g0[8], x0[8], y0[8];
+    load8_bf16(dy + o0, g0);
+    load8_bf16(x + o0, x0);
+    if constexpr (RELU) load8_bf16(y + o0, y0);
+    finish(g0, x0, y0, o0);
   }
 }
 
@@ -296,13 +359,15 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
   DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
                                                     momentum, eps, coef, nullptr, nullptr);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
-      else bn_apply_kernel<T, true, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
     } else {
-      if (relu) bn_apply_kernel<T, false, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
-      else bn_apply_kernel<T, false, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
     }
   });
 }
@@ -325,13 +390,15 @@ void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
   float* coef = ws;
   bn_infer_coef_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, rmean, rvar, eps, C, coef);
   dim3 grid(g.nchunk, g.gy);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
-      else bn_apply_kernel<T, true, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
     } else {
-      if (relu) bn_apply_kernel<T, false, true><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
-      else bn_apply_kernel<T, false, false><<<grid, kBlk, 0, st>>>(x, res, y, coef, M, C, g.rows_per_chunk);
+      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
     }
   });
 }
@@ -350,13 +417,15 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr, nullptr,
                                                     const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
                                                     coef, dgamma, dbeta);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (relu) {
-      if (dres) bn_bwd_dx_kernel<T, true, true><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
-      else bn_bwd_dx_kernel<T, true, false><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+      if (dres) bn_bwd_dx_kernel<T, true, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
+      else bn_bwd_dx_kernel<T, true, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
     } else {
-      if (dres) bn_bwd_dx_kernel<T, false, true><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
-      else bn_bwd_dx_kernel<T, false, false><<<grid, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, g.rows_per_chunk);
+      if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
+      else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
     }
   });
 }
