@@ -8,11 +8,11 @@
 //   reductions across the 16 lanes that share a row) -> dropout(P) through a per-wave LDS
 //   scratch into A-fragment layout -> O += P V (8 MFMA).  Writes O (bf16, coalesced through LDS) and
 //   LSE = m + log(l) per row for the backward.  No [S, S] matrix ever reaches HBM.
-// Backward (grid: [B*nh], 4 waves; a wave owns 32 keys; S <= 128):
+// Backward (grid: [B*nh], 8 waves; a wave owns 16 keys; S in {64, 128}):
 //   recomputes P^T = exp(K Q^T * scale + mask - LSE) per 32-query chunk, then
-//   dV += dropout(P)^T dO,  dP^T = V dO^T,  dS^T = P^T (dropout'(dP^T) - D),  dK += dS^T Q * scale,
-//   dQ += dS K * scale (LDS fp32 accumulator shared by the 4 key-waves, ds_add),
-//   with D = rowsum(dO * O) computed in the prologue.  40 MFMA per wave per chunk.
+//   dV += dropout(P)^T dO,  dP^T = V dO^T,  dS^T = P^T (dropout'(dP^T) - D),  dK += dS^T Q * scale;
+//   dS^T is kept whole in LDS, so after one barrier dQ = dS K * scale is a plain MFMA pass per
+//   16-query wave (no atomics).  D = rowsum(dO * O) is computed in the prologue.
 //
 // Fragment conventions as in dtg/mfma_gemm.cuh: mfma(a = X_A[m][k], b = X_B[n][k]) accumulates
 // C[m][n], lane l holding C[(l>>4)*4 + r][l & 15].
@@ -22,7 +22,6 @@
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
-#include <stdlib.h>
 
 namespace dtg {
 using namespace gemm;
@@ -191,13 +190,44 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Backward, S <= 128 (one workgroup holds a whole (b, h)).  LDS: Q, dO, K as MC tiles (S/64 x 8 KB
-// each), dQ fp32 [S][64], D and LSE [S], per-wave scratch 2 x [32][32] bf16.
-__global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+// Backward, S in {64, 128}: one workgroup (8 waves) per (b, h); wave w owns keys [16w, 16w+16).
+// LDS (S = 128: 90 KB): Q, dO, K as MC tiles (ds_read_b64_tr_b16 B-operands), the whole dS^T
+// [S keys][S q] bf16 (written by the key-waves, read back transposed for dQ = dS K -- no atomics),
+// D / LSE / mask rows, and per-wave [16 keys][32 q] scratch for dropout(P)^T.
+//   phase 1 (per 32-query chunk): S^T = K Q^T, dP^T = V dO^T (16 MFMA) -> P^T, dropout, dS^T
+//            -> dV += Pd^T dO, dK += dS^T Q (8 MFMA)
+//   phase 2 (after a barrier): wave w computes dQ for query rows [16w, 16w+16) over all keys.
+// Gradients leave through LDS staging as 16-byte row stores.
+template <int S_>
+__device__ __forceinline__ int dst_off(int key, int q) {  // dS^T [key][q], MC-swizzled 2*S_-byte rows
+  return key * (S_ * 2) + ((((q >> 3) ^ mc_swz<S_ / 8>(key))) << 4) + (q & 7) * 2;
+}
+
+// rows [row0, row0+16) x 64 bf16 of a wave's C-layout accumulators -> global (16-B stores) via a
+// 2 KB per-wave LDS staging area
+__device__ __forceinline__ void store_rows16(lds_char* stg, const f32x4 (&v)[4], float scale, bf16_t* g, long long ldg,
+                                             int lane) {
+  const int rbase = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st_bf16(stg, (rbase + r) * 128 + (j * 16 + (lane & 15)) * 2, v[j][r] * scale);
+  lds_fence();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = lane + 64 * i, row = c >> 3, ch = c & 7;
+    const v8bf x = *reinterpret_cast<const lds_v8bf*>(stg + row * 128 + ch * 16);
+    *reinterpret_cast<v8bf*>(g + row * ldg + ch * 8) = x;
+  }
+  lds_fence();
+}
+
+template <int S_>
+__global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                        const bf16_t* __restrict__ dout, const float* __restrict__ lse,
                                                        const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
-                                                       int S, int nh, float scale, uint32_t th, float dscale,
-                                                       uint32_t seed, int abl) {
+                                                       int nh, float scale, uint32_t th, float dscale, uint32_t seed) {
+  constexpr int S = S_, NW = 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
   const int H = nh * 64;
@@ -209,29 +239,27 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
   const bf16_t* Vg = Qg + 2 * H;
   const bf16_t* Og = o + (long long)b * S * H + h * 64;
   const bf16_t* dOg = dout + (long long)b * S * H + h * 64;
-  const int nc64 = S / 64;
-  lds_char* Qt = smem;                        // MC [q][d]
-  lds_char* dOt = Qt + S * 128;               // MC [q][d]
-  lds_char* Kt = dOt + S * 128;               // MC [key][d]
-  lds_float* dQs = reinterpret_cast<lds_float*>(Kt + S * 128);  // [S][64] fp32
-  lds_float* Ds = dQs + S * 64;               // [S]
-  lds_float* Ls = Ds + S;                     // [S]
-  lds_float* Ms = Ls + S;                     // [S] key mask
-  lds_char* scrP = reinterpret_cast<lds_char*>(Ms + S) + wave * 4096;  // [32 keys][32 q] MC-swizzled
-  lds_char* scrS = scrP + 2048;
+  lds_char* Qt = smem;                         // MC [q][d]
+  lds_char* dOt = Qt + S * 128;                // MC [q][d]
+  lds_char* Kt = dOt + S * 128;                // MC [key][d]
+  lds_char* dST = Kt + S * 128;                // [S][S] bf16
+  lds_float* Ds = reinterpret_cast<lds_float*>(dST + S * S * 2);
+  lds_float* Ls = Ds + S;
+  lds_float* Ms = Ls + S;
+  lds_char* scr = reinterpret_cast<lds_char*>(Ms + S) + wave * 1024;  // [16 keys][32 q]
   {
     DenseMC<false> qs_{Qg, ld, 64, S};
     DenseMC<false> ds_{dOg, (long long)H, 64, S};
     DenseMC<false> kss{Kg, ld, 64, S};
-    for (int c = 0; c < nc64; ++c) {
-      stage_mc<64>(qs_, Qt + c * 8192, 0, c * 64, wave, lane);
-      stage_mc<64>(ds_, dOt + c * 8192, 0, c * 64, wave, lane);
-      stage_mc<64>(kss, Kt + c * 8192, 0, c * 64, wave, lane);
+#pragma unroll
+    for (int c = 0; c < S / 64; ++c) {
+      stage_mc<64, DenseMC<false>, NW>(qs_, Qt + c * 8192, 0, c * 64, wave, lane);
+      stage_mc<64, DenseMC<false>, NW>(ds_, dOt + c * 8192, 0, c * 64, wave, lane);
+      stage_mc<64, DenseMC<false>, NW>(kss, Kt + c * 8192, 0, c * 64, wave, lane);
     }
   }
-  // D[q] = sum_d dO[q, d] * O[q, d]  (two threads per row, 32 columns each), LSE, key mask, dQ = 0
-  for (int i = tid; i < ((abl & 1) ? 0 : 2 * S); i += 256) {
-    const int q = i >> 1, half = i & 1;
+  if (tid < 2 * S) {  // D[q] = sum_d dO[q, d] * O[q, d]: two threads per row
+    const int q = tid >> 1, half = tid & 1;
     float acc = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -244,135 +272,92 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(const bf16_t* __restrict_
     acc += __shfl_xor(acc, 1, 64);
     if (half == 0) Ds[q] = acc;
   }
-  if (abl & 1)
-    for (int i = tid; i < S; i += 256) Ds[i] = 0.f;
-  for (int i = tid; i < S; i += 256) {
-    Ls[i] = lse[(long long)bh * S + i];
-    Ms[i] = mask ? mask[(long long)b * S + i] : 0.f;
+  if (tid < S) {
+    Ls[tid] = lse[(long long)bh * S + tid];
+    Ms[tid] = mask ? mask[(long long)b * S + tid] : 0.f;
   }
-  for (int i = tid; i < S * 64; i += 256) dQs[i] = 0.f;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int rbase = (lane >> 4) * 4;
-  for (int kb = wave * 32; kb < S; kb += 128) {  // this wave's 32-key block(s)
-    v8bf ka[2][2], va[2][2];
+  const int kb = wave * 16;
+  const bool has_keys = kb < S;
+  f32x4 dk[4], dv[4];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        ka[mi][ks] = gfrag(Kg, ld, kb + mi * 16, ks, lane);
-        va[mi][ks] = gfrag(Vg, ld, kb + mi * 16, ks, lane);
-      }
-    f32x4 dk[2][4], dv[2][4];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dk[mi][j] = dv[mi][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) dk[j] = dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (has_keys) {
+    const v8bf ka0 = gfrag(Kg, ld, kb, 0, lane), ka1 = gfrag(Kg, ld, kb, 1, lane);
+    const v8bf va0 = gfrag(Vg, ld, kb, 0, lane), va1 = gfrag(Vg, ld, kb, 1, lane);
+#pragma unroll 1
     for (int qc = 0; qc < S; qc += 32) {
-      const int tq = qc >> 6, kq = (qc & 63) >> 5;  // 64-row MC tile and its 32-row half
-      // sT[key][q] = K Q^T ; dPdT[key][q] = V dO^T
-      f32x4 st[2][2], dpt[2][2];
+      const int tq = qc >> 6, kq = (qc & 63) >> 5;
+      f32x4 st[2], dpt[2];
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        v8bf qb0, qb1, db0, db1;
-        if (abl & 8) {
-          qb0 = ka[0][0]; qb1 = ka[0][1]; db0 = va[0][0]; db1 = va[0][1];
-        } else {
-          qb0 = gfrag(Qg, ld, qc + ni * 16, 0, lane); qb1 = gfrag(Qg, ld, qc + ni * 16, 1, lane);
-          db0 = gfrag(dOg, (long long)H, qc + ni * 16, 0, lane); db1 = gfrag(dOg, (long long)H, qc + ni * 16, 1, lane);
-        }
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[mi][0], qb0, z, 0, 0, 0);
-          st[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[mi][1], qb1, z, 0, 0, 0);
-          z = f32x4{0.f, 0.f, 0.f, 0.f};
-          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[mi][0], db0, z, 0, 0, 0);
-          dpt[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[mi][1], db1, z, 0, 0, 0);
-        }
-      }
-      // P^T, dropout, dS^T  (C layout: row = key, col = q)
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int qcol = ni * 16 + (lane & 15);
-          const int q = qc + qcol;
-          const float lq = Ls[q], dq = Ds[q];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int krow = mi * 16 + rbase + r;
-            const int key = kb + krow;
-            const float p = __expf(st[mi][ni][r] * scale + Ms[key] - lq);
-            float pd = p, dp = dpt[mi][ni][r];
-            if (th) {
-              const bool kp = keep_elem(seed, (uint32_t)(((long long)bh * S + q) * S + key), th);
-              pd = kp ? p * dscale : 0.f;
-              dp = kp ? dp * dscale : 0.f;
-            }
-            st_bf16(scrP, mc32_off(krow, qcol), pd);
-            st_bf16(scrS, mc32_off(krow, qcol), p * (dp - dq));
-          }
-        }
-      lds_fence();
-      // A fragments [key][q] (one 16-B chunk per lane) and the transposed dS [q][key] (tr reads)
-      v8bf pa[2], sa[2], sta[2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const int krow = mi * 16 + (lane & 15), ch = lane >> 4;
-        const int off = krow * 64 + ((ch ^ mc_swz<4>(krow)) << 4);
-        pa[mi] = *reinterpret_cast<const lds_v8bf*>(scrP + off);
-        sa[mi] = *reinterpret_cast<const lds_v8bf*>(scrS + off);
-        sta[mi] = frag_mc<32>(scrS, mi * 16, 0, lane);  // X_A[q][key] = dS
+        const v8bf qb0 = gfrag(Qg, ld, qc + ni * 16, 0, lane), qb1 = gfrag(Qg, ld, qc + ni * 16, 1, lane);
+        const v8bf db0 = gfrag(dOg, (long long)H, qc + ni * 16, 0, lane);
+        const v8bf db1 = gfrag(dOg, (long long)H, qc + ni * 16, 1, lane);
+        f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka0, qb0, z, 0, 0, 0);
+        st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka1, qb1, z, 0, 0, 0);
+        z = f32x4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va0, db0, z, 0, 0, 0);
+        dpt[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va1, db1, z, 0, 0, 0);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const v8bf dob = frag_mc<64>(dOt + tq * 8192, j * 16, kq, lane);  // X_B[d][q] = dO
-        const v8bf qbm = frag_mc<64>(Qt + tq * 8192, j * 16, kq, lane);   // X_B[d][q] = Q
-        const v8bf kbm = frag_mc<64>(Kt + (kb >> 6) * 8192, j * 16, (kb & 63) >> 5, lane);  // X_B[d][key] = K
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          dv[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[mi], dob, dv[mi][j], 0, 0, 0);
-          dk[mi][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[mi], qbm, dk[mi][j], 0, 0, 0);
-          f32x4 dq = f32x4{0.f, 0.f, 0.f, 0.f};
-          dq = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sta[mi], kbm, dq, 0, 0, 0);
-          if (abl & 2) {
-            asm volatile("" ::"v"(dq[0]), "v"(dq[1]), "v"(dq[2]), "v"(dq[3]));
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              __builtin_amdgcn_ds_faddf(dQs + (qc + mi * 16 + rbase + r) * 64 + j * 16 + (lane & 15), dq[r], 0, 0,
-                                        false);
-          }
-        }
-      }
-      lds_fence();  // scratch reuse by the next chunk
-    }
-    // dK (scaled), dV -> dqkv
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int ni = 0; ni < 2; ++ni) {
+        const int qcol = ni * 16 + (lane & 15), q = qc + qcol;
+        const float lq = Ls[q], dq = Ds[q];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const long long row = (long long)b * S + kb + mi * 16 + rbase + r;
-          const int col = h * 64 + j * 16 + (lane & 15);
-          if (abl & 4) {
-            asm volatile("" ::"v"(dk[mi][j][r]), "v"(dv[mi][j][r]));
-          } else {
-            dqkv[row * ld + H + col] = f2bf(dk[mi][j][r] * scale);
-            dqkv[row * ld + 2 * H + col] = f2bf(dv[mi][j][r]);
+          const int krow = rbase + r, key = kb + krow;
+          const float p = __expf(st[ni][r] * scale + Ms[key] - lq);
+          float pd = p, dp = dpt[ni][r];
+          if (th) {
+            const bool kp = keep_elem(seed, (uint32_t)(((long long)bh * S + q) * S + key), th);
+            pd = kp ? p * dscale : 0.f;
+            dp = kp ? dp * dscale : 0.f;
           }
+          st_bf16(scr, mc32_off(krow, qcol), pd);
+          st_bf16(dST, dst_off<S>(key, q), p * (dp - dq));
         }
-  }
-  __syncthreads();
-  for (int i = tid; i < S * 8; i += 256) {  // dQ: 8 x 16-B chunks per row
-    const int q = i >> 3, ch = i & 7;
-    float v[8];
+      }
+      lds_fence();
+      const int key_l = lane & 15, ch = lane >> 4;
+      const v8bf pa = *reinterpret_cast<const lds_v8bf*>(scr + key_l * 64 + ((ch ^ mc_swz<4>(key_l)) << 4));
+      const int key = kb + key_l, qch = (qc >> 3) + ch;
+      const v8bf sa = *reinterpret_cast<const lds_v8bf*>(dST + key * (S * 2) + ((qch ^ mc_swz<S / 8>(key)) << 4));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = dQs[q * 64 + ch * 8 + k] * scale;
-    store8_bf16(dqkv + ((long long)b * S + q) * ld + h * 64 + ch * 8, v);
+      for (int j = 0; j < 4; ++j) {
+        dv[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_mc<64>(dOt + tq * 8192, j * 16, kq, lane), dv[j], 0,
+                                                        0, 0);
+        dk[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, frag_mc<64>(Qt + tq * 8192, j * 16, kq, lane), dk[j], 0,
+                                                        0, 0);
+      }
+      lds_fence();  // scratch rewritten by the next chunk
+    }
+  }
+  __syncthreads();  // dS^T complete; Q / dO tiles free for output staging
+  lds_char* stg = smem + wave * 2048;  // inside the Q / dO tiles (16 or 32 KB)
+  if (has_keys) {
+    bf16_t* gk = dqkv + ((long long)b * S + kb) * ld + H + h * 64;
+    store_rows16(stg, dk, scale, gk, ld, lane);
+    store_rows16(stg, dv, 1.f, gk + H, ld, lane);
+  }
+  const int qr = wave * 16;
+  if (qr < S) {
+    f32x4 dq[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < S / 32; ++kk) {
+      const v8bf a = frag_mc<S>(dST, qr, kk, lane);  // X_A[q][key] = dS
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        dq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, frag_mc<64>(Kt + (kk >> 1) * 8192, j * 16, kk & 1, lane),
+                                                        dq[j], 0, 0, 0);
+    }
+    store_rows16(stg, dq, scale, dqkv + ((long long)b * S + qr) * ld + h * 64, ld, lane);
   }
 }
 
@@ -384,11 +369,11 @@ static uint32_t drop_th(float p) {
 
 int attn_fused_supported(int S, int dh, int backward) {
   if (dh != 64 || S % 64 != 0 || S <= 0) return 0;
-  return backward ? (S <= 128) : (S <= 512);
+  return backward ? (S == 64 || S == 128) : (S <= 512);
 }
 
 static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + 4 * 2048; }
-static size_t bwd_lds(int S) { return (size_t)3 * S * 128 + (size_t)S * 64 * 4 + 3 * S * 4 + 4 * 4096; }
+static size_t bwd_lds(int S) { return (size_t)3 * S * 128 + (size_t)S * S * 2 + 3 * S * 4 + 8 * 1024; }
 
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,
               uint32_t seed, hipStream_t st) {
@@ -407,11 +392,20 @@ void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int
 
 void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, const float* mask,
               bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, hipStream_t st) {
-  static const int abl = getenv("DTG_ATTN_ABL") ? atoi(getenv("DTG_ATTN_ABL")) : 0;  // perf ablation only
   const uint32_t th = drop_th(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(B * nh), dim3(256), bwd_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                     0.125f, th, ds, seed, abl);
+  static bool attr = false;
+  if (!attr) {
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel<128>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds(128)));
+    attr = true;
+  }
+  if (S == 64)
+    hipLaunchKernelGGL(attn_bwd_kernel<64>, dim3(B * nh), dim3(512), bwd_lds(64), st, qkv, o, dout, lse, mask, dqkv,
+                       nh, 0.125f, th, ds, seed);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<128>, dim3(B * nh), dim3(512), bwd_lds(128), st, qkv, o, dout, lse, mask,
+                       dqkv, nh, 0.125f, th, ds, seed);
 }
 
 }  // namespace dtg
