@@ -84,6 +84,10 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
   }
 }
 
+// 256x256 8-wave 8-phase GEMM (gemm8.hip); same operand conventions as gemm_bf16, no batching
+void gemm8_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, const Epi& e,
+                int M, int N, int K, int split_k, int kps, float* ws, hipStream_t st);
+
 // split-K reduction of fp32 slabs [split][M][N] + the epilogue (gemm.hip)
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st);
 

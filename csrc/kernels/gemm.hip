@@ -183,6 +183,17 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   }
 }
 
+// 256x256 / 8-wave / 8-phase kernel (gemm8.hip) for GEMMs big enough to fill the chip with 256x256
+// tiles; DTG_GEMM8=0/1 forces it off/on (A/B runs).
+static bool use_8phase(int M, int N, int K, int split_k) {
+  if (const char* f = getenv("DTG_GEMM8")) {
+    if (f[0] == '0') return false;
+    if (f[0] == '1') return M >= 256 && N >= 128;
+  }
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256) * split_k;
+  return split_k == 1 && M >= 256 && N >= 256 && K >= 256 && tiles >= 240;
+}
+
 // 256x128 tile, 8 waves, one workgroup per CU, 3-slot LDS ring with counted vmcnt (prefetch
 // distance 2).  Chosen when the grid still fills the chip with these larger tiles and K per block
 // is long enough for the deeper pipeline to matter.
@@ -224,6 +235,10 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
+  if (bt.count == 1 && use_8phase(M, N, K, split_k)) {
+    gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
+    return;
+  }
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else if (use_big(M, N, kps, split_k, bt)) launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);

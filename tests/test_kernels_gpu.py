@@ -278,3 +278,25 @@ def test_gemm_big_tile_ring(M, N, K, a_kc, b_kc, monkeypatch):
     assert ((out - ref).norm() / ref.norm()).item() < 1e-2
     out2 = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=3)
     assert ((out2 - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 64), (512, 768, 128), (1024, 512, 192), (768, 1024, 1024),
+                                   (1000, 600, 328), (256, 256, 512)])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
+def test_gemm_8phase(M, N, K, a_kc, b_kc, monkeypatch):
+    """256x256 8-wave 8-phase kernel (forced on) vs fp32 torch: 1, 2, 3 and many K-tiles, ragged edges,
+    all four operand layouts, bias + GELU epilogue, split-K slabs."""
+    monkeypatch.setenv("DTG_GEMM8", "1")
+    torch.manual_seed(0)
+    A = torch.randn((M, K) if a_kc else (K, M), device="cuda").bfloat16()
+    B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()
+    bias = torch.randn(N, device="cuda")
+    ref = (A.float() if a_kc else A.float().t()) @ (B.float().t() if b_kc else B.float()) + bias
+    out = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=1)
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+    outg = ops.gemm(A, a_kc, B, b_kc, bias=bias, act="gelu", split_k=1)
+    refg = F.gelu(ref, approximate="tanh")
+    assert ((outg.float() - refg).norm() / refg.norm()).item() < 2e-2
+    if K >= 256:
+        out2 = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=2)
+        assert ((out2 - ref).norm() / ref.norm()).item() < 1e-2
