@@ -190,8 +190,10 @@ static bool use_8phase(int M, int N, int K, int split_k) {
     if (f[0] == '0') return false;
     if (f[0] == '1') return M >= 256 && N >= 128;
   }
-  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256) * split_k;
-  return split_k == 1 && M >= 256 && N >= 256 && K >= 256 && tiles >= 240;
+  // measured (profiles/r01_gemm8): wins once a 256x256 block has >= 8 K-tiles of work and the grid
+  // carries >= ~200k tile*K; loses at K = 256 (prologue/epilogue dominated) and on <= 96 short tiles
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  return split_k == 1 && M >= 256 && N >= 256 && K >= 512 && tiles >= 96 && tiles * K >= 196608;
 }
 
 // 256x128 tile, 8 waves, one workgroup per CU, 3-slot LDS ring with counted vmcnt (prefetch
