@@ -25,7 +25,7 @@ import time
 import torch
 import torch.distributed as dist
 
-_GRAD, _DONE = 1, 2
+_GRAD, _DONE, _ELASTIC = 1, 2, 3
 
 
 def _group_payload_grads(flat):
@@ -151,13 +151,45 @@ class AsyncPSServer:
 
     def _handle(self, w):
         """Header from worker w has landed: DONE -> False; else receive, apply, reply -> True."""
-        if int(self._hdr[w][0].item()) == _DONE:
+        kind = int(self._hdr[w][0].item())
+        if kind == _DONE:
             return False
+        if kind == _ELASTIC:
+            self._elastic(w)
+            return True
         for b in self._recv[w]:
             dist.recv(b, src=w, group=self.pg)
         self._apply(w)
         self._send_params(w)
         return True
+
+    def _elastic(self, w):
+        """EASGD exchange (Zhang, Choromanska, LeCun 2015): receive the worker's parameters x_i,
+        d = alpha * (x_i - x~), x~ += d, send d back (the worker applies x_i -= d)."""
+        bufs = self._recv_elastic[w]
+        for b in bufs:
+            dist.recv(b, src=w, group=self.pg)
+        with torch.no_grad():
+            for g, b in zip(self.flat, bufs):
+                b.sub_(g.master).mul_(self.elastic_alpha)
+                g.master.add_(b)
+                g.refresh_mirror()
+        for prev in self._send_works[w]:
+            prev.wait()
+        snap = self._snap_elastic[w]
+        for s_, b in zip(snap, bufs):
+            s_.copy_(b)
+        self._send_works[w] = [dist.isend(s_, dst=w, group=self.pg) for s_ in snap]
+        self.version += 1
+        self.updates += 1
+        self.per_worker[w] += 1
+
+    def enable_elastic(self, alpha):
+        """Serve EASGD exchanges: the PS parameters are the elastic center variable x~."""
+        self.elastic_alpha = float(alpha)
+        self._recv_elastic = {w: [torch.empty_like(g.master) for g in self.flat] for w in self.workers}
+        self._snap_elastic = {w: [torch.empty_like(g.master) for g in self.flat] for w in self.workers}
+        return self
 
     def serve(self, poll_sleep=0.0):
         for w in self.workers:
@@ -198,6 +230,63 @@ class AsyncPSServer:
             self._hdr[w].copy_(hdr)
             if not self._handle(w):
                 live.discard(w)
+
+
+class ElasticWorker:
+    """Asynchronous elastic-averaging SGD worker (AEASGD; AEAMSGD with a momentum local optimizer) --
+    the algorithms the reference lists as TODO (README.md:40-42, paper link README.md:99).
+
+    The worker trains its own replica x_i with ``local_optimizer`` every step; every ``tau`` steps it
+    exchanges with the PS center x~:  d = alpha (x_i - x~);  x_i -= d;  x~ += d  (moving-average
+    coupling instead of gradient pushes; the PS must call ``AsyncPSServer.enable_elastic(alpha)``).
+    """
+
+    def __init__(self, flat, local_optimizer, tau=4, ps_rank=0, group=None):
+        self.flat = flat
+        self.opt = local_optimizer
+        self.tau = max(1, int(tau))
+        self.ps = ps_rank
+        self.pg = group
+        dev = next(iter(flat)).master.device
+        self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self._d = [torch.empty_like(g.master) for g in flat]
+        self.local_step = 0
+        self.exchanges = 0
+
+    def begin(self):
+        """Start from the center: receive the PS parameters (mirror / fp32 group) into the replica."""
+        for buf in _group_payload_params(self.flat):
+            dist.recv(buf, src=self.ps, group=self.pg)
+        with torch.no_grad():
+            for g in self.flat:
+                if g.mirror is not None:
+                    g.master.copy_(g.mirror)
+
+    def step_done(self):
+        """After backward: local optimizer step; every tau steps an elastic exchange."""
+        self.local_step += 1
+        self.opt.step()
+        if self.local_step % self.tau:
+            return False
+        self._hdr[0] = _ELASTIC
+        self._hdr[1] = self.local_step
+        dist.send(self._hdr, dst=self.ps, group=self.pg)
+        works = [dist.isend(g.master, dst=self.ps, group=self.pg) for g in self.flat]
+        for w in works:
+            w.wait()
+        for d in self._d:
+            dist.recv(d, src=self.ps, group=self.pg)
+        with torch.no_grad():
+            for g, d in zip(self.flat, self._d):
+                g.master.sub_(d)
+                g.refresh_mirror()
+        self.exchanges += 1
+        return True
+
+    def finish(self):
+        self._hdr[0] = _DONE
+        self._hdr[1] = self.local_step
+        dist.send(self._hdr, dst=self.ps, group=self.pg)
 
 
 def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1):

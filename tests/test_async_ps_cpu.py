@@ -151,3 +151,92 @@ def test_async_ps_two_workers_hogwild():
     for r in (1, 2):
         ls = out[r]["losses"]
         assert ls[-1] < ls[0], ls
+
+
+def _elastic_rank(rank, world, port, steps, tau, alpha, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import dtg  # noqa: F401
+        from dtg import ops
+        from dtg.optim import FusedSGD
+        from dtg.parallel import FlatParams, comm
+        from dtg.parallel.async_ps import AsyncPSServer, ElasticWorker
+        comm.init("gloo")
+        model = _model()
+        flat = FlatParams(model, compute_dtype=torch.float32)
+        if rank == 0:
+            ps = AsyncPSServer(flat, None, workers=range(1, world)).enable_elastic(alpha)
+            n = ps.serve()
+            q.put((rank, "ok", {"updates": n, "w": [g.master.clone() for g in flat]}))
+        else:
+            w = ElasticWorker(flat, FusedSGD(flat, lr=0.1, momentum=0.0), tau=tau)
+            w.begin()
+            x, y = _data(rank)
+            losses = []
+            for _ in range(steps):
+                loss = ops.softmax_cross_entropy(model(x), y)
+                loss.backward()
+                w.step_done()
+                losses.append(loss.item())
+            w.finish()
+            q.put((rank, "ok", {"losses": losses, "exchanges": w.exchanges}))
+        comm.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+        raise
+
+
+def _run_elastic(world, steps, tau, alpha):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_elastic_rank, args=(r, world, port, steps, tau, alpha, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, status, payload = q.get(timeout=240)
+        assert status == "ok", status
+        out[r] = payload
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+def test_easgd_single_worker_matches_replay():
+    """AEASGD (reference README TODO): with one worker the exchanges are sequential -> exact replay."""
+    steps, tau, alpha = 12, 3, 0.5
+    out = _run_elastic(2, steps, tau, alpha)
+    assert out[0]["updates"] == steps // tau and out[1]["exchanges"] == steps // tau
+    import dtg  # noqa: F401
+    from dtg import ops
+    model = _model()
+    center = {n: p.detach().clone() for n, p in model.named_parameters()}
+    x, y = _data(1)
+    params = dict(model.named_parameters())
+    for i in range(steps):
+        loss = ops.softmax_cross_entropy(model(x), y)
+        grads = torch.autograd.grad(loss, list(params.values()))
+        with torch.no_grad():
+            for p, g in zip(params.values(), grads):
+                p.sub_(0.1 * g)
+            if (i + 1) % tau == 0:
+                for n, p in params.items():
+                    d = alpha * (p - center[n])
+                    p.sub_(d)
+                    center[n].add_(d)
+    got = _ps_params_by_name(out)
+    for n, v in center.items():
+        assert torch.allclose(got[n], v, atol=1e-5), n
+
+
+def test_easgd_two_workers_learn():
+    out = _run_elastic(3, 24, 4, 0.3)
+    assert out[0]["updates"] == 2 * (24 // 4)
+    for r in (1, 2):
+        assert out[r]["losses"][-1] < out[r]["losses"][0]

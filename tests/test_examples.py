@@ -158,3 +158,51 @@ def test_non_distributed_gap_factor():
     assert len(vals) == 100
     ratio = (100 - vals[-1]) / (100 - vals[0])
     assert abs(ratio - 0.9998 ** 990) < 1e-4  # gap shrinks by (1 - 2 lr) per step; it does not converge
+
+
+def _aeasgd_oracle(steps_global, tau, alpha, lr, momentum=0.0):
+    """One worker, sequential: local (momentum-)SGD on c = a + b -> 100, elastic coupling every tau."""
+    import numpy as np
+    a = np.zeros(2, np.float64)
+    b = np.zeros(2, np.float64)
+    ca, cb = a.copy(), b.copy()
+    ma, mb = np.zeros(2), np.zeros(2)
+    gs = 0
+    while gs < steps_global:
+        for _ in range(tau):
+            g = (a + b - 100.0)  # d/da mean((a+b-100)^2) over 2 elements = 2(c-100)/2
+            if momentum > 0:
+                ma = momentum * ma + g
+                mb = momentum * mb + g
+                a, b = a - lr * ma, b - lr * mb
+            else:
+                a, b = a - lr * g, b - lr * g
+        da, db = alpha * (a - ca), alpha * (b - cb)
+        a, b = a - da, b - db
+        ca, cb = ca + da, cb + db
+        gs += 1
+    return a + b, ca + cb
+
+
+def test_aeasgd_single_worker_matches_oracle():
+    from _cluster import run_cluster
+    out = run_cluster("AEASGD/AEASGD.py", n_ps=1, n_workers=1,
+                      args=["--tau", "3", "--alpha", "0.5", "--lr", "0.1", "--last_step", "8"])
+    rc, o = out[("worker", 0)]
+    assert rc == 0, o
+    c_local, c_center = _aeasgd_oracle(8, 3, 0.5, 0.1)
+    center_line = [l for l in o.splitlines() if l.startswith("center")][-1]
+    vals = [float(x) for x in center_line.split("[")[1].split("]")[0].split()]
+    assert abs(vals[0] - c_center[0]) < 1e-3 * max(1.0, abs(c_center[0])), (vals, c_center)
+
+
+def test_aemasgd_two_workers_converge():
+    from _cluster import run_cluster
+    out = run_cluster("AEASGD/AEASGD.py", n_ps=1, n_workers=2,
+                      args=["--tau", "2", "--alpha", "0.3", "--lr", "0.05", "--momentum", "0.5", "--last_step", "30"])
+    for t in range(2):
+        rc, o = out[("worker", t)]
+        assert rc == 0, o
+    center_line = [l for l in out[("worker", 0)][1].splitlines() if l.startswith("center")][-1]
+    vals = [float(x) for x in center_line.split("[")[1].split("]")[0].split()]
+    assert all(abs(v - 100.0) < 5.0 for v in vals), vals
