@@ -7,16 +7,18 @@
 //     A_h = rows {128 wr + 64 h + [0, 64)}  (the h-th 64-row quarter of both wave-row slabs)
 //     B_h = cols {64 wc + 32 h + [0, 32)}   (the h-th 32-col half of every wave's column block)
 // Phases per K-tile compute one (mq, nq) quadrant (64x32 per wave, 16 MFMA) in the order
-//     P0 (0,0): ds_read A_0, B_0     P1 (1,0): ds_read A_1     P2 (1,1): ds_read B_1     P3 (0,1): ds_read A_0
-// so each half of buffer u&1 dies at a known phase (B_0 @P0, A_1 @P1, B_1 @P2, A_0 @P3) and is
-// re-staged (LDS-DMA, 2 glds per thread per half) for a later tile two phases after it dies:
-//     tile u issues  P0: B_1(u+1)  P1: A_0(u+1)  P2: B_0(u+2)  P3: A_1(u+2)
-// Each phase = { ds_read; glds; s_barrier; lgkmcnt(0); setprio 1; 16 MFMA; setprio 0; [P2: counted
-// vmcnt]; s_barrier }.  Waves 4-7 run one barrier behind waves 0-3 (one extra s_barrier up front),
-// so on every SIMD one wave is in its MFMA section while the other is in its load section.  With
-// that stagger a DMA is published to all readers two phases after the issuing waves' vmcnt, and a
-// half can be overwritten two phases after its last read -- the schedule above satisfies both; the
-// single wait per K-tile (end of P2: everything but the newest half retired) covers every read.
+//     P0 (0,0): ds_read A_0, B_0     P1 (1,0): ds_read A_1     P2 (1,1): ds_read B_1     P3 (0,1): -
+// (A_0's fragments stay in registers until P3), so every half of buffer u&1 is read in exactly one
+// phase (A_0, B_0 @P0, A_1 @P1, B_1 @P2) and is re-staged (LDS-DMA, 2 glds per thread per half) for
+// a later tile at least two phases after that read:
+//     tile u issues  P0: A_1(u+1)  P1: B_1(u+1)  P2: A_0(u+2)  P3: B_0(u+2)
+// giving every half >= 3 phases of DMA flight.  Each phase = { ds_read; glds; s_barrier; lgkmcnt(0);
+// setprio 1; 16 MFMA; setprio 0; counted vmcnt; s_barrier }.  Waves 4-7 run one barrier behind
+// waves 0-3 (one extra s_barrier up front), so on every SIMD one wave is in its MFMA section while
+// the other is in its load section.  With that stagger a DMA is visible to every reader two phases
+// after the issuing waves' vmcnt, and a half can be overwritten two phases after its last read: the
+// waits at the end of P0 / P2 / P3 retire exactly the halves read two phases later and leave the
+// three newest halves (vmcnt 6) in flight; the tail counts are exact.
 // All LDS is one __shared__ array (a second LDS object can make hipcc drain vmcnt each step).
 #include "dtg/common.h"
 #include "dtg/kernels.h"
@@ -104,36 +106,40 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(SA sa, SB sb, int M, int 
   auto stB = [&](int u, int h) { g8::stage_half<BKC, false>(sb, B_h(u, h), bn0, h, kbeg + u * BK, wave, lane); };
 
   if (nk > 0) {
-    // prologue: all of tile 0, then the halves of tile 1 that steady state issues one tile early
+    // prologue: tile 0 plus the two tile-1 halves steady state issues two phases before tile 0
+    // starts; retire A_0, B_0, A_1 of tile 0 (needed by P0/P1), keep 3 halves in flight
     stA(0, 0);
     stB(0, 0);
     stA(0, 1);
     stB(0, 1);
     if (nk > 1) {
+      stA(1, 0);
       stB(1, 0);
-      stA(1, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed, tile 1's two halves in flight
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();  // raw barrier: __syncthreads would drain the in-flight DMA
     if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger: waves 4-7 run one barrier behind
 
-    v8bf a[4][2], b[2][2];
+    // A_0 fragments stay in registers from P0 to P3 (a0), A_1 from P1 to P2 (a1), so every half is
+    // read from LDS in exactly one phase and can be re-staged early (>= 3 phases of DMA flight)
+    v8bf a0[4][2], a1[4][2], b[2][2];
     for (int u = 0; u < nk; ++u) {
-      // ---- P0: quadrant (0,0): read A_0, B_0; issue B_1(u+1)
+      const bool n1 = u + 1 < nk, n2 = u + 2 < nk;
+      // ---- P0: quadrant (0,0): read A_0, B_0; issue A_1(u+1); retire B_1(u)
       {
         const lds_char* ta = A_h(u, 0);
         const lds_char* tb = B_h(u, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) a[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
+          for (int ks = 0; ks < 2; ++ks) a0[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) b[j][ks] = g8::hfrag<BKC>(tb, wc * 32 + j * 16, ks, lane);
-        if (u + 1 < nk) stB(u + 1, 1);
+        if (n1) stA(u + 1, 1);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
@@ -143,18 +149,20 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(SA sa, SB sb, int M, int 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i][ks], b[j][ks], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
+        if (n1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
-      // ---- P1: quadrant (1,0): read A_1; issue A_0(u+1)
+      // ---- P1: quadrant (1,0): read A_1; issue B_1(u+1)
       {
         const lds_char* ta = A_h(u, 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) a[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
-        if (u + 1 < nk) stA(u + 1, 0);
+          for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
+        if (n1) stB(u + 1, 1);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
@@ -164,18 +172,18 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(SA sa, SB sb, int M, int 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
-              acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[4 + i][j], 0, 0, 0);
+              acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i][ks], b[j][ks], acc[4 + i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_s_barrier();
       }
-      // ---- P2: quadrant (1,1): read B_1; issue B_0(u+2); then retire all but the newest half
+      // ---- P2: quadrant (1,1): read B_1; issue A_0(u+2); retire A_0(u+1), B_0(u+1)
       {
         const lds_char* tb = B_h(u, 1);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) b[j][ks] = g8::hfrag<BKC>(tb, wc * 32 + j * 16, ks, lane);
-        if (u + 2 < nk) stB(u + 2, 0);
+        if (n2) stA(u + 2, 0);
         __builtin_amdgcn_s_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
@@ -186,22 +194,16 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(SA sa, SB sb, int M, int 
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
               acc[4 + i][2 + j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[4 + i][2 + j], 0, 0, 0);
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i][ks], b[j][ks], acc[4 + i][2 + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        if (u + 2 < nk) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
-      // ---- P3: quadrant (0,1): read A_0; issue A_1(u+2)
+      // ---- P3: quadrant (0,1): registers only (a0, B_1); issue B_0(u+2); retire A_1(u+1)
       {
-        const lds_char* ta = A_h(u, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) a[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
-        if (u + 2 < nk) stA(u + 2, 1);
+        if (n2) stB(u + 2, 0);
         __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -209,8 +211,10 @@ __global__ void __launch_bounds__(512, 1) gemm8_kernel(SA sa, SB sb, int M, int 
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks)
-              acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[i][2 + j], 0, 0, 0);
+              acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i][ks], b[j][ks], acc[i][2 + j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
+        if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       }
     }
