@@ -124,11 +124,12 @@ std::vector<c10::optional<Tensor>> ln_bwd(Tensor dy, Tensor s, Tensor gamma, Ten
   }
   c10::DeviceGuard dg(s.device());
   auto ds = at::empty_like(s);
+  auto ws = at::empty({(long long)dtg::ln_bwd_blocks(T) * 3 * H}, s.options().dtype(at::kFloat));
   c10::optional<Tensor> dh;
   if (want_dh) dh = p_in > 0 ? at::empty_like(s) : ds;
   dtg::ln_bwd(cbfp(dy), cbfp(s), gamma.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), bfp(ds),
               (want_dh && p_in > 0) ? bfp(*dh) : nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-              has(dbias) ? dbias->data_ptr<float>() : nullptr, T, (int)H, (float)p_in, (uint32_t)seed_in, (float)p_out, (uint32_t)seed_out,
+              has(dbias) ? dbias->data_ptr<float>() : nullptr, ws.data_ptr<float>(), T, (int)H, (float)p_in, (uint32_t)seed_in, (float)p_out, (uint32_t)seed_out,
               cur_stream());
   return {ds, dh};
 }

@@ -58,9 +58,10 @@ int ln_max_hidden();
 void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,
             float* mean, float* rstd, int T, int H, float eps, float p_in, uint32_t seed_in, float p_out,
             uint32_t seed_out, hipStream_t st);
+int ln_bwd_blocks(int T);  // ln_bwd workspace = ln_bwd_blocks(T) * 3H floats
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* dbias, int T, int H, float p_in,
-            uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st);
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* dbias, float* ws, int T, int H,
+            float p_in, uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st);
 int attn_max_keys();
 void attn_softmax_fwd(const float* sc, const float* mask, bf16_t* P, bf16_t* Pd, int rows, int rows_per_b, int Sk,
                       float p, uint32_t seed, hipStream_t st);

@@ -190,10 +190,18 @@ static bool use_8phase(int M, int N, int K, int split_k) {
     if (f[0] == '0') return false;
     if (f[0] == '1') return M >= 256 && N >= 128;
   }
-  // measured (profiles/r01_gemm8): wins once a 256x256 block has >= 8 K-tiles of work and the grid
-  // carries >= ~200k tile*K; loses at K = 256 (prologue/epilogue dominated) and on <= 96 short tiles
-  const long long tiles = (long long)((M + 255) / 256) * ((N + 255) / 256);
-  return split_k == 1 && M >= 256 && N >= 256 && K >= 512 && tiles >= 96 && tiles * K >= 196608;
+  // Both kernels run one "round" of tiles at a time (256x256: 1 workgroup per CU; 128x128: 2 per
+  // CU), so compare round utilisation, crediting the 8-phase kernel with its per-CU advantage, which
+  // grows with K (measured, profiles/r01_gemm8: ~1.15x at K = 768 in a cold-cache training step, up
+  // to ~2x at K >= 2048); it loses at K = 256 (prologue/epilogue dominated).
+  if (split_k != 1 || M < 256 || N < 256 || K < 512) return false;
+  const long long t8 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
+  if (t8 < 48) return false;
+  const double u8 = (double)t8 / (double)(((t8 + 255) / 256) * 256);
+  const double u128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
+  const double gain = K >= 2048 ? 2.1 : (K >= 1024 ? 1.4 : 1.15);
+  return u8 * gain > u128;
 }
 
 // 256x128 tile, 8 waves, one workgroup per CU, 3-slot LDS ring with counted vmcnt (prefetch

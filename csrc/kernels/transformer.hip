@@ -113,14 +113,14 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 // ---- LayerNorm backward ----------------------------------------------------------------------------
 // g = dropout_out'(dy); ds = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat))
 // ds_out = ds (the residual-branch gradient); dh_out = dropout_in'(ds) (the branch gradient);
-// per-block sums of g*xhat and g are added to dgamma/dbeta with fp32 atomics (one per column
-// per block; the grid is capped so the contention per address stays small).
+// per-block sums of g*xhat, g (and the branch gradient, for the fused bias grad) are written as
+// partial rows and folded by ln_param_reduce_kernel.
 template <int NCH>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds_out,
-                                                     bf16_t* __restrict__ dh_out, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, float* __restrict__ dbias, int T, int H,
+                                                     bf16_t* __restrict__ dh_out, float* __restrict__ ws,
+                                                     float* __restrict__ dbias, int T, int H,
                                                      uint32_t th_in, float sc_in, uint32_t seed_in, uint32_t th_out,
                                                      float sc_out, uint32_t seed_out) {
   extern __shared__ float red[];  // [4][3H]: gamma, beta, branch-bias partials
@@ -190,12 +190,44 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
       }
   }
   __syncthreads();
+  // per-block partials of [dgamma | dbeta | dbias] -> ws[block][3H]; ln_param_reduce_kernel sums them
   const int nred = dbias ? 3 * H : 2 * H;
   for (int i = threadIdx.x; i < nred; i += blockDim.x) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kRowsPerBlock; ++w) t += red[w * 3 * H + i];
-    atomicAdd(i < H ? dgamma + i : (i < 2 * H ? dbeta + (i - H) : dbias + (i - 2 * H)), t);
+    ws[(long long)blockIdx.x * 3 * H + i] = t;
+  }
+}
+
+// out[i] += sum over the nb partial rows of ws[:, i]  (i < ncols; out = [dgamma | dbeta | dbias]).
+// Grid (ncols/64, 8 row groups); block = 64 columns x 4 row lanes; a row group folds its rows with
+// 8 loads in flight per thread, then one atomic per column per group (8-way, not nb-way).
+__global__ void __launch_bounds__(256) ln_param_reduce_kernel(const float* __restrict__ ws, int nb, int H,
+                                                              int ncols, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, float* __restrict__ dbias) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lr = threadIdx.x >> 6;
+  const int per = (nb + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(nb, r0 + per);
+  float t = 0.f;
+  if (col < ncols) {
+    int r = r0 + lr;
+    for (; r + 28 < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = ws[(long long)(r + 4 * k) * 3 * H + col];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += v[k];
+    }
+    for (; r < r1; r += 4) t += ws[(long long)r * 3 * H + col];
+  }
+  red[lr][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (lr == 0 && col < ncols) {
+    t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(col < H ? dgamma + col : (col < 2 * H ? dbeta + (col - H) : dbias + (col - 2 * H)), t);
   }
 }
 
@@ -290,7 +322,20 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __res
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[v][k] = 0.f;
   if (ok) {
-    for (int r = blockIdx.y * 8 + rl; r < T; r += gridDim.y * 8) {
+    const int step = gridDim.y * 8;
+    int r = blockIdx.y * 8 + rl;
+    if (!sel) {  // bias grads: 4 rows per iteration, four 16-B loads in flight
+      for (; r + 3 * step < T; r += 4 * step) {
+        float t0[8], t1[8], t2[8], t3[8];
+        load8_bf16(x + (long long)r * ld + c * 8, t0);
+        load8_bf16(x + (long long)(r + step) * ld + c * 8, t1);
+        load8_bf16(x + (long long)(r + 2 * step) * ld + c * 8, t2);
+        load8_bf16(x + (long long)(r + 3 * step) * ld + c * 8, t3);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[0][k] += (t0[k] + t1[k]) + (t2[k] + t3[k]);
+      }
+    }
+    for (; r < T; r += step) {
       float t[8];
       load8_bf16(x + (long long)r * ld + c * 8, t);
       const int v = sel ? (int)sel[r] : 0;
@@ -437,8 +482,8 @@ int ln_bwd_blocks(int T) {
 }
 
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
-            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* dbias, int T, int H, float p_in,
-            uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st) {
+            bf16_t* ds_out, bf16_t* dh_out, float* dgamma, float* dbeta, float* dbias, float* ws, int T, int H,
+            float p_in, uint32_t seed_in, float p_out, uint32_t seed_out, hipStream_t st) {
   if (T <= 0) return;
   const uint32_t ti = drop_thresh(p_in), to = drop_thresh(p_out);
   const float si = p_in > 0.f ? 1.f / (1.f - p_in) : 1.f, so = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
@@ -447,11 +492,14 @@ void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* 
   const size_t lds = (size_t)kRowsPerBlock * 3 * H * sizeof(float);
 #define DTG_LNB(NC)                                                                                                  \
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
-                     dgamma, dbeta, dbias, T, H, ti, si, seed_in, to, so, seed_out)
+                     ws, dbias, T, H, ti, si, seed_in, to, so, seed_out)
   if (nch <= 1) DTG_LNB(1);
   else if (nch == 2) DTG_LNB(2);
   else DTG_LNB(4);
 #undef DTG_LNB
+  const int ncols = dbias ? 3 * H : 2 * H;
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((ncols + 63) / 64, 8), dim3(256), 0, st, ws, nb, H, ncols, dgamma,
+                     dbeta, dbias);
 }
 
 int attn_max_keys() { return 64 * 16; }
