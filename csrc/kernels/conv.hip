@@ -291,7 +291,7 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   const int M = N * G.P * G.Q, No = R * S * C;
-  const long long tiles = (long long)((K + 127) / 128) * ((No + 127) / 128);
+  const long long tiles = K <= 64 ? (long long)((No + 255) / 256) : (long long)((K + 127) / 128) * ((No + 127) / 128);
   int s = 1;
   while (tiles * s < 512 && (long long)M / (s * 2) >= 1024 && s < 256) s *= 2;
   return s;
@@ -304,11 +304,15 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
   int kps = (M + split - 1) / split;
   kps = (kps + BK - 1) / BK * BK;
   split = (M + kps - 1) / kps;
-  using CF = Cfg<128, 128, 2>;
-  const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
-  dim3 grid(tm * tn, split);
   Epi e{dw, No, dw_bf16, 1.f, beta, nullptr, 0};
-  conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
+  auto run = [&](auto cf) {
+    using CF = decltype(cf);
+    const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
+    dim3 grid(tm * tn, split);
+    conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
+  };
+  if (K <= 64) run(Cfg<64, 256, 2>());  // 64 output channels: one 64-row tile, no wasted MFMA rows
+  else run(Cfg<128, 128, 2>());
   gemm_splitk_reduce(ws, split, K, No, e, st);
 }
 

@@ -132,8 +132,10 @@ long long gemm_workspace_floats(int M, int N, int K, int split_k) {
 
 static bool skinny(int N) { return N <= 64; }
 
+static bool short_m(int M, int N) { return M <= 64 && N >= 128; }
+
 int gemm_pick_split(int M, int N, int K) {
-  const int BMv = skinny(N) ? 256 : 128, BNv = skinny(N) ? 64 : 128;
+  const int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   int s = 1;
   // aim for >= ~512 workgroups (2 per CU: the LDS ring admits 2) while keeping >= 1024 K
@@ -250,6 +252,8 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     return;
   }
   if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else if (short_m(M, N))  // 64-row weight gradients (64-channel layers): no half-empty 128-row tiles
+    launch_cfg<64, 256>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else if (use_big(M, N, kps, split_k, bt)) launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
 }

@@ -300,3 +300,16 @@ def test_gemm_8phase(M, N, K, a_kc, b_kc, monkeypatch):
     if K >= 256:
         out2 = ops.gemm(A, a_kc, B, b_kc, bias=bias, out_dtype=torch.float32, split_k=2)
         assert ((out2 - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,a_kc,b_kc", [(64, 256, 8192, False, False), (64, 576, 4096, False, False),
+                                             (48, 300, 512, True, True), (64, 1024, 256, True, False)])
+def test_gemm_short_m_tiles(M, N, K, a_kc, b_kc):
+    """M <= 64 (64-channel weight gradients) runs on 64x256 tiles, with and without split-K."""
+    torch.manual_seed(0)
+    A = torch.randn((M, K) if a_kc else (K, M), device="cuda").bfloat16()
+    B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()
+    ref = (A.float() if a_kc else A.float().t()) @ (B.float().t() if b_kc else B.float())
+    for sk in (1, 0):
+        out = ops.gemm(A, a_kc, B, b_kc, out_dtype=torch.float32, split_k=sk)
+        assert ((out - ref).norm() / ref.norm()).item() < 1e-2, sk
