@@ -332,7 +332,9 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad) {
   return y;
 }
 
-Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad) {
+// dx (= or +=, beta) dgrad; `out` (optional, [N,H,W,C] bf16) receives it in place
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, c10::optional<Tensor> out,
+                  double beta) {
   check_nhwc(dy, "dy");
   check_nhwc(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -341,8 +343,16 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 1), "dgrad shape not supported by the HIP kernel");
   TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q, "dgrad geometry mismatch");
   c10::DeviceGuard dg(dy.device());
-  auto dx = at::empty({N, H, W, C}, dy.options());
-  dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, cur_stream());
+  Tensor dx;
+  if (out.has_value()) {
+    dx = *out;
+    check_nhwc(dx, "out");
+    TORCH_CHECK(dx.size(0) == N && dx.size(1) == H && dx.size(2) == W && dx.size(3) == C, "out shape mismatch");
+  } else {
+    TORCH_CHECK(beta == 0.0, "beta != 0 needs out");
+    dx = at::empty({N, H, W, C}, dy.options());
+  }
+  dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, (float)beta, cur_stream());
   return dx;
 }
 
@@ -374,7 +384,9 @@ void register_pool_ops(pybind11::module_& m);         // pool_ops.cc
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_supported", &conv_supported);
   m.def("conv_fwd", &conv_fwd);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"), pybind11::arg("W"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("out") = pybind11::none(),
+        pybind11::arg("beta") = 0.0);
   m.def("conv_wgrad", &conv_wgrad);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);

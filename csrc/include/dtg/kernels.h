@@ -98,12 +98,12 @@ void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, 
             hipStream_t st);
 
 // ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
-// which: 0 fwd, 1 dgrad, 2 wgrad
+// which: 0 fwd, 1 dgrad, 2 wgrad.  Strided dgrad runs one dense launch per residue class of dx.
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
               int stride, int pad, hipStream_t st);
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-                int stride, int pad, hipStream_t st);
+                int stride, int pad, float beta, hipStream_t st);
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad);
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
                 int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st);

@@ -14,6 +14,8 @@
 // Requirements (checked on the host): C % 64 == 0 and K % 64 == 0 (a 64-deep K-step then stays inside
 // one filter tap, so the tap is uniform per step and only the row/channel part is per lane).
 // Out-of-image taps read the zero page; row/column clamps keep every address inside its tensor.
+#include <algorithm>
+
 #include "dtg/common.h"
 #include "dtg/gemm_epi.cuh"
 #include "dtg/kernels.h"
@@ -174,6 +176,92 @@ struct WgradB {
   }
 };
 
+// ---- strided dgrad: one residue class (h % st, w % st) of dx per launch --------------------------
+// For stride st the input row h = st*i + ph only receives the taps r = r0 + st*tr (r0 = (ph+pad) mod
+// st), from dy row p = i + dh - tr (dh = (ph + pad - r0) / st).  Each residue class is therefore a
+// dense stride-1 problem over (n, i, j) x (tr, ts, k) -- no MFMA work is spent on the zero taps the
+// st^2-times-larger "dilated dy" formulation would multiply.
+struct StrideClass {
+  int ph, pw, r0, s0, nr, ns, Hc, Wc, dh, dw, tiles;
+  FastDiv fHWc, fWc, fNS;
+};
+// all residue classes of one dgrad go out in ONE launch (blockIdx.y = class, heaviest first) so the
+// small classes fill the CUs the big ones leave idle instead of each being a sub-wave launch
+constexpr int kMaxClasses = 9;
+struct StrideClasses {
+  StrideClass c[kMaxClasses];
+};
+
+template <int ROWS>
+struct DgradSA {
+  static constexpr int PW = ROWS / 32;
+  const bf16_t* dy;
+  const ConvGeom* g;
+  const StrideClass* sc;
+  int nbase[PW], pi[PW], qj[PW];
+  int cx;
+  __device__ __forceinline__ void init(const ConvGeom& G, const StrideClass& S, const bf16_t* dyp, int row0, int wave,
+                                       int lane) {
+    dy = dyp;
+    g = &G;
+    sc = &S;
+    const int M = G.N * S.Hc * S.Wc;
+    cx = (lane & 7) ^ (lane >> 3);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      int m = row0 + (wave * PW + i) * 8 + (lane >> 3);
+      m = m < M ? m : M - 1;
+      uint32_t n, ij, ii, jj;
+      S.fHWc.divmod((uint32_t)m, n, ij);
+      S.fWc.divmod(ij, ii, jj);
+      nbase[i] = (int)n * G.P;
+      pi[i] = (int)ii + S.dh;
+      qj[i] = (int)jj + S.dw;
+    }
+  }
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave) const {
+    uint32_t t, k0c, tr, ts;
+    g->fK.divmod((uint32_t)k0, t, k0c);
+    sc->fNS.divmod(t, tr, ts);
+    const int ch = (int)k0c + cx * 8;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int p = pi[i] - (int)tr, q = qj[i] - (int)ts;
+      const bool ok = (unsigned)p < (unsigned)g->P && (unsigned)q < (unsigned)g->Q;
+      const int pc = ok ? p : 0, qc = ok ? q : 0;
+      const void* src = sel(ok, dy + ((long long)(nbase[i] + pc) * g->Q + qc) * g->K + ch);
+      const int r0 = (wave * PW + i) * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + r0 * 128), 16, 0, 0);
+    }
+  }
+};
+
+template <int ROWS>
+struct DgradSB {
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  const bf16_t* w;
+  const ConvGeom* g;
+  const StrideClass* sc;
+  int col0;
+  __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave, int lane) const {
+    uint32_t t, kb, tr, ts;
+    g->fK.divmod((uint32_t)k0, t, kb);
+    sc->fNS.divmod(t, tr, ts);
+    const int rs = (sc->r0 + g->stride * (int)tr) * g->S + sc->s0 + g->stride * (int)ts;
+    const long long rsc = (long long)g->R * g->S * g->C;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int kr0 = (wave * PW + i) * KPI;
+      const int kr = kr0 + lane / CH;
+      const int c = (lane % CH) ^ mc_swz<CH>(kr);
+      const int col = col0 + c * 8;
+      const bool ok = col < g->C;
+      const void* src = sel(ok, w + (long long)((int)kb + kr) * rsc + (long long)rs * g->C + (ok ? col : 0));
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + kr0 * ROWS * 2), 16, 0, 0);
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------------------------
 template <class CF>
 __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
@@ -247,12 +335,43 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   });
 }
 
+template <class CF>
+__global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideClasses SC,
+                                                             const bf16_t* __restrict__ dy,
+                                                             const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
+  lds_char* smem = (lds_char*)smem_raw;
+  const StrideClass S = SC.c[blockIdx.y];
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t >= S.tiles) return;
+  const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int M = G.N * S.Hc * S.Wc, Kd = S.nr * S.ns * G.K;
+  DgradSA<CF::BM> sa;
+  sa.init(G, S, dy, bm0, wave, lane);
+  DgradSB<CF::BN> sb{w, &G, &S, bn0};
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
+                               [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) {
+    uint32_t nn, ij, ii, jj;
+    S.fHWc.divmod((uint32_t)m, nn, ij);
+    S.fWc.divmod(ij, ii, jj);
+    const int row = ((int)nn * G.H + G.stride * (int)ii + S.ph) * G.W + G.stride * (int)jj + S.pw;
+    epi_store8(e, G.C, row, n, v);
+  });
+}
+
 // ---------------------------------------------------------------------------------------------
 static bool conv_skinny(int n) { return n <= 64; }
 
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
   if (C % 64 || K % 64) return 0;
-  if (which == 1 && stride != 1) return 0;  // dgrad: stride-1 only (strided dgrad -> library)
+  if (which == 1 && stride * stride > kMaxClasses) return 0;  // one launch holds <= 9 residue classes
   return 1;
 }
 
@@ -272,11 +391,59 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   }
 }
 
+static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
+                               hipStream_t st) {
+  const int s = G.stride;
+  bool empty = false;
+  for (int ph = 0; ph < s; ++ph)
+    for (int pw = 0; pw < s; ++pw) {
+      const int r0 = ((ph + G.pad) % s + s) % s, s0 = ((pw + G.pad) % s + s) % s;
+      if (r0 >= G.R || s0 >= G.S || ph >= G.H || pw >= G.W) empty = true;
+    }
+  if (empty && beta == 0.f) {  // residue classes no tap reaches are zero
+    DTG_HIP_CHECK(hipMemsetAsync(dx, 0, (size_t)G.N * G.H * G.W * G.C * sizeof(bf16_t), st));
+    beta = 1.f;
+  }
+  Epi e{dx, G.C, 1, 1.f, beta, nullptr, 0};
+  const bool skinny = conv_skinny(G.C);
+  const int BM = skinny ? 256 : 128, BN = skinny ? 64 : 128;
+  const int tn = (G.C + BN - 1) / BN;
+  StrideClasses SC;
+  int nc = 0, max_tiles = 0;
+  for (int ph = 0; ph < s; ++ph)
+    for (int pw = 0; pw < s; ++pw) {
+      StrideClass S;
+      S.ph = ph; S.pw = pw;
+      S.r0 = ((ph + G.pad) % s + s) % s;
+      S.s0 = ((pw + G.pad) % s + s) % s;
+      if (S.r0 >= G.R || S.s0 >= G.S || ph >= G.H || pw >= G.W) continue;
+      S.nr = (G.R - S.r0 + s - 1) / s;
+      S.ns = (G.S - S.s0 + s - 1) / s;
+      S.Hc = (G.H - ph + s - 1) / s;
+      S.Wc = (G.W - pw + s - 1) / s;
+      S.dh = (ph + G.pad - S.r0) / s;
+      S.dw = (pw + G.pad - S.s0) / s;
+      S.fHWc = FastDiv(S.Hc * S.Wc); S.fWc = FastDiv(S.Wc); S.fNS = FastDiv(S.ns);
+      S.tiles = (G.N * S.Hc * S.Wc + BM - 1) / BM * tn;
+      max_tiles = S.tiles > max_tiles ? S.tiles : max_tiles;
+      SC.c[nc++] = S;
+    }
+  if (nc == 0) return;
+  // heaviest residue class (most taps) first: blocks dispatch in y-major order
+  std::stable_sort(SC.c, SC.c + nc, [](const StrideClass& a, const StrideClass& b) {
+    return a.nr * a.ns > b.nr * b.ns;
+  });
+  const dim3 grid(max_tiles, nc);
+  if (skinny) conv_dgrad_s_kernel<Cfg<256, 64, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+  else conv_dgrad_s_kernel<Cfg<128, 128, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+}
+
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-                int stride, int pad, hipStream_t st) {
+                int stride, int pad, float beta, hipStream_t st) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+  if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st);
   const int M = N * H * W;
-  Epi e{dx, C, 1, 1.f, 0.f, nullptr, 0};
+  Epi e{dx, C, 1, 1.f, beta, nullptr, 0};
   if (conv_skinny(C)) {
     using CF = Cfg<256, 64, 2>;
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;

@@ -12,7 +12,8 @@ Everything runs on dtg's HIP kernels on [rows, channels] views of NHWC activatio
             the flat gradient buffer and BN gamma/beta gradients are accumulated in the BN
             finalize kernel -- autograd sees no parameter gradients at all, the all-reduce
             buckets are notified through parallel/grad_sink.
-Strided 3x3 dgrad goes to MIOpen (channels_last, no layout conversion).
+Strided dgrads (3x3/s2 and the 1x1/s2 projection) run dtg's residue-class dgrad kernel; the
+projection's accumulates (beta = 1) straight into the conv1 dgrad output.
 """
 import torch
 
@@ -105,15 +106,11 @@ class _BottleneckFn(torch.autograd.Function):
         # BN2 + conv2 (3x3)
         dy2, _, _, _ = L.bn_bwd(da2, a2, y2, b2.weight, m2, i2, True, False, g[id(b2.weight)], g[id(b2.bias)])
         dy2_4 = dy2.view(n, p_, q_, width)
-        if st == 1:
-            da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, 1, 1).view(-1, width)
-        else:
-            gi = torch.ops.aten.convolution_backward(dy2_4.permute(0, 3, 1, 2), a1.view(n, h, w, width).permute(
-                0, 3, 1, 2), w2, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
-            da1 = _rows(gi)
+        da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
         L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
         # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
         dy1, _, _, _ = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])
+        dx_done = False
         if blk.down is not None:
             yd, md, idd = sv[13:16]
             bd, wd = blk.down.bn, blk.down.conv.weight
@@ -123,15 +120,16 @@ class _BottleneckFn(torch.autograd.Function):
                 dx2 = gemm(dyd, True, _mat(wd), False)
                 gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
             else:
-                dsub = gemm(dyd, True, _mat(wd), False).view(n, p_, q_, c)
-                dx4 = torch.zeros(n, h, w, c, device=x2.device, dtype=x2.dtype)
-                dx4[:, ::st, ::st, :] = dsub
-                dx2 = dx4.view(-1, c)
+                dx2 = gemm(dy1, True, _mat(w1), False)
+                L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0, out=dx2.view(n, h, w, c),
+                             beta=1.0)
+                dx_done = True
                 L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
                              st, 0)
         else:
             dx2 = dres
-        gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
+        if not dx_done:
+            gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
         gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
         grads = []
         for p, (a, direct) in zip(params, accs):

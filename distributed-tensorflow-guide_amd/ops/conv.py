@@ -4,7 +4,7 @@ Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
   * 1x1 / stride 1 / pad 0 -> the MFMA GEMM (csrc/kernels/gemm.hip) on the [N*H*W, C] row view:
         fwd  Y  = X  W^T      dgrad dX = dY W      wgrad dW = dY^T X
   * k x k, C % 64 == 0, K % 64 == 0 -> implicit-GEMM conv (csrc/kernels/conv.hip):
-        fwd and wgrad at any stride, dgrad at stride 1 (strided dgrad -> MIOpen)
+        fwd, dgrad and wgrad at any stride (strided dgrad: one dense launch per residue class of dx)
   * small channel counts (C % 64 != 0, K % 8 == 0: MNIST's 1/32-channel convs) -> im2col kernel +
     MFMA GEMM with the bias/ReLU epilogue; dgrad = GEMM + col2im gather kernel
     (``conv2d_bias_act``)
@@ -91,7 +91,7 @@ class _ConvImplicit(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if lib().conv_supported(c, k, r, s, st, pad, 1):
                 dx = lib().conv_dgrad(dy4, w4.contiguous(), h, wd, st, pad).permute(0, 3, 1, 2)
-            else:  # strided dgrad: MIOpen
+            else:  # unsupported channel counts: MIOpen
                 w_cl = w4.permute(0, 3, 1, 2)
                 dx = torch.nn.grad.conv2d_input(ctx.xshape, w_cl, dy4.permute(0, 3, 1, 2), st, pad)
         p = ctx.param

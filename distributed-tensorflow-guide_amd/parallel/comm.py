@@ -19,11 +19,19 @@ def init(backend=None, timeout_s=600):
 
     Returns (rank, local_rank, world, device)."""
     rank, local, world = env_rank()
+    # DTG_BACKEND=gloo with DTG_GLOO_DEVICE=cuda rehearses the multi-rank GPU path on ONE card
+    # (several ranks share cuda:0; gloo stages the collectives through host memory) -- RCCL
+    # refuses two ranks on one device, so this is how the bucket/hook/grad-sink path is tested on a
+    # one-GPU box.  Production runs leave both unset (RCCL, one GPU per rank).
+    backend = os.environ.get("DTG_BACKEND") or backend
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
+    elif os.environ.get("DTG_GLOO_DEVICE") == "cuda" and torch.cuda.is_available():
+        device = torch.device("cuda", local % torch.cuda.device_count())
+        torch.cuda.set_device(device)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():

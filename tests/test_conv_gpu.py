@@ -22,6 +22,10 @@ CASES = [
     (3, 64, 128, 9, 3, 1, 1),      # odd spatial size, partial tiles
     (2, 256, 512, 14, 1, 2, 0),    # 1x1 stride-2 downsample
     (2, 128, 64, 7, 3, 1, 1),      # skinny N (fwd) / skinny C (dgrad)
+    (2, 64, 128, 7, 3, 2, 1),      # strided dgrad, odd size: unequal residue classes, skinny C
+    (2, 128, 64, 9, 1, 2, 0),      # 1x1/s2 dgrad, odd size: odd residue classes get no tap (zeros)
+    (2, 64, 64, 10, 3, 3, 1),      # stride 3
+    (2, 64, 64, 12, 5, 2, 2),      # 5x5 stride 2
 ]
 
 
@@ -62,3 +66,22 @@ def test_conv_direct_grad_into_flat_buffer():
     assert g.data_ptr() >= flat.groups["compute"].grad.data_ptr()
     assert _rel(g, 2 * wr.grad) < 3e-2
     assert ref_w.shape == g.shape
+
+
+@pytest.mark.parametrize("R,st,pad,H", [(3, 2, 1, 56), (1, 2, 0, 28), (3, 2, 1, 15)])
+def test_conv_dgrad_strided_accumulate(R, st, pad, H):
+    """Residue-class dgrad with beta = 1 into an existing buffer (the ResNet projection path)."""
+    from dtg.ops._native import lib
+    g = torch.Generator(device="cpu").manual_seed(R * 100 + H)
+    N, C, K = 2, 128, 256
+    P = (H + 2 * pad - R) // st + 1
+    dy = torch.randn(N, P, P, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    base = torch.randn(N, H, H, C, generator=g).to(DEV, torch.bfloat16)
+    out = base.clone()
+    lib().conv_dgrad(dy, w, H, H, st, pad, out=out, beta=1.0)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dy.float().permute(0, 3, 1, 2),
+                                     st, pad).permute(0, 2, 3, 1)
+    assert _rel(out, base.float() + ref) < 1e-2
+    fresh = lib().conv_dgrad(dy, w, H, H, st, pad)
+    assert _rel(fresh, ref) < 1e-2
