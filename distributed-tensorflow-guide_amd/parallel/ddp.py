@@ -69,19 +69,31 @@ class DataParallel:
         self._reset()
 
     # -- hooks ---------------------------------------------------------------------------------
+    # A parameter counts towards its bucket exactly once per backward.  Direct-write ops
+    # (grad_sink.notify) report from inside their backward; autograd ALSO runs the parameter's
+    # AccumulateGrad node afterwards (with an undefined gradient, since the op returned None) and
+    # that fires the post-accumulate hook a second time -- it must not count again, or a bucket
+    # would launch its all-reduce while some of its gradients are still being computed.
     def _reset(self):
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
+        self._done = set()
 
     def _launch(self, b):
         b.work = dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _on_direct(self, p):
         if p in self._param_bucket:
-            self._on_grad(p)
+            self._count(p)
 
     def _on_grad(self, p):
+        self._count(p)
+
+    def _count(self, p):
+        if p in self._done:
+            return
+        self._done.add(p)
         b = self._param_bucket[p]
         b.pending -= 1
         if b.pending == 0:

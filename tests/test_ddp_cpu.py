@@ -88,3 +88,81 @@ def test_allreduce_dp_equivalence_two_ranks():
         p.join(120)
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: "ok", 1: "ok"}, res
+
+
+class _DirectMul(__import__("torch").autograd.Function):
+    """y = x * w with w's gradient written straight into its flat view + grad_sink.notify (the
+    fused GPU ops' contract); returns None for w, so autograd still runs w's AccumulateGrad."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x * w
+
+    @staticmethod
+    def backward(ctx, dy):
+        from dtg.parallel import grad_sink
+        x, w = ctx.saved_tensors
+        w.grad.add_((dy * x).sum(0))
+        grad_sink.notify(w)
+        return dy * w, None
+
+
+def _rank_direct(rank, world, port, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import dtg  # noqa: F401
+        from dtg.parallel import DataParallel, FlatParams, comm
+        comm.init("gloo")
+
+        class M(torch.nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.ws = torch.nn.ParameterList([torch.nn.Parameter(torch.full((64,), 1.0 + i)) for i in range(4)])
+
+            def forward(self, x):
+                for w in self.ws:
+                    x = _DirectMul.apply(x, w)
+                return x
+
+        model = M()
+        flat = FlatParams(model, compute_dtype=torch.float32, keep_fp32=lambda n, p: False)
+        dp = DataParallel(flat, bucket_mb=1.0)  # ONE bucket holding all four parameters
+        assert len(dp.buckets) == 1
+        launched_with = []
+        real_launch = dp._launch
+
+        def spy(b):
+            launched_with.append(len(dp._done))
+            real_launch(b)
+        dp._launch = spy
+        x = torch.ones(2, 64) * (rank + 1)
+        for _ in range(2):  # twice: the per-step bookkeeping must reset
+            flat.zero_grad()
+            model(x).sum().backward()
+            dp.finish()
+        # the bucket's all-reduce may only start once all four gradients are written
+        assert launched_with == [4, 4], launched_with
+        comm.shutdown()
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_direct_write_params_count_once():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_direct, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: "ok", 1: "ok"}, res
