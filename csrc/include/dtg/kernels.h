@@ -46,6 +46,8 @@ struct GemmBatch {
   int count = 1, nh = 1;
   long long sa_b = 0, sa_h = 0, sb_b = 0, sb_h = 0, sc_b = 0, sc_h = 0;
 };
+// force one GEMM tile configuration (sweeps; 0 = heuristic, 99 = 8-phase 256x256)
+void gemm_force_cfg(int cfg);
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
 int gemm_pick_split(int M, int N, int K);
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,

@@ -49,6 +49,7 @@ struct Cfg {
   static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_, NW = NW_, NTH = NW_ * 64;
   static constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == NW, "one 64x64 sub-tile per wave");
+  static_assert(STAGES >= 1 && STAGES <= 5, "ring depth");
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
@@ -214,31 +215,38 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
       compute_tile<C, AKC, BKC>(smem, smem + C::A_BYTES, wm, wn, lane, acc);
       __syncthreads();
     }
-  } else if constexpr (C::STAGES == 3) {
-    // 3-slot ring, prefetch distance 2, one barrier per K-step.  At the top of step kt the wave's
-    // outstanding LDS-DMA ops are those of tiles kt and kt+1 (LPS each): a counted vmcnt(LPS)
-    // retires tile kt only, the barrier publishes it to all waves (and certifies every wave is done
-    // reading slot (kt+2)%3 = (kt-1)%3), then tile kt+2's DMA is issued and tile kt computed.
+  } else if constexpr (C::STAGES >= 3) {
+    // S-slot ring, prefetch distance D = S-1, one barrier per K-step.  At the top of step kt the
+    // wave's outstanding LDS-DMA ops are those of tiles kt .. min(kt+D-1, nk-1) (LPS each, issued
+    // in order; vmcnt retires in issue order): a counted vmcnt(younger*LPS) retires tile kt only,
+    // the barrier publishes it to all waves (and certifies every wave is done reading slot
+    // (kt+D)%S = (kt-1)%S), then tile kt+D's DMA is issued and tile kt computed.  Deep rings keep
+    // (S-1) stages of operand bytes in flight per workgroup: what the memory-bound short-K GEMMs
+    // need (bandwidth = bytes in flight / latency).
+    constexpr int S = C::STAGES, D = S - 1;
     constexpr int LPS = stage_loads<C::BM, C::NW>() + stage_loads<C::BN, C::NW>();
-    sta(smem, kbeg);
-    stb(smem + C::A_BYTES, kbeg);
-    if (nk > 1) {
-      sta(smem + C::STAGE_BYTES, kbeg + BK);
-      stb(smem + C::STAGE_BYTES + C::A_BYTES, kbeg + BK);
-    }
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+      if (i < nk) {
+        sta(smem + i * C::STAGE_BYTES, kbeg + i * BK);
+        stb(smem + i * C::STAGE_BYTES + C::A_BYTES, kbeg + i * BK);
+      }
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int younger = min(D - 1, nk - 1 - kt);
+      if constexpr (D - 1 >= 3) { if (younger >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory"); }
+      if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+      else if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (kt + 2 < nk) {
-        const int s2 = slot >= 1 ? slot - 1 : 2;  // (kt + 2) % 3
-        sta(smem + s2 * C::STAGE_BYTES, kbeg + (kt + 2) * BK);
-        stb(smem + s2 * C::STAGE_BYTES + C::A_BYTES, kbeg + (kt + 2) * BK);
+      if (kt + D < nk) {
+        const int sd = slot == 0 ? S - 1 : slot - 1;  // (kt + D) % S
+        sta(smem + sd * C::STAGE_BYTES, kbeg + (kt + D) * BK);
+        stb(smem + sd * C::STAGE_BYTES + C::A_BYTES, kbeg + (kt + D) * BK);
       }
       compute_tile<C, AKC, BKC>(smem + slot * C::STAGE_BYTES, smem + slot * C::STAGE_BYTES + C::A_BYTES, wm, wn, lane,
                                 acc);
-      slot = slot == 2 ? 0 : slot + 1;
+      slot = slot == S - 1 ? 0 : slot + 1;
     }
   } else {
     sta(smem, kbeg);

@@ -225,6 +225,52 @@ static void launch_big(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
 }
 
+template <class CF>
+static void launch_exact(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
+                         int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
+                         const GemmBatch& bt) {
+  const bool full = (M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0);
+  if (full) launch_layout<CF, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+}
+
+// DTG_GEMM_CFG=<n> forces one tile configuration (tools/gemm_sweep.py A/B sweeps); 0 = heuristic
+static int g_forced_cfg = -1;
+static int forced_cfg() {
+  if (g_forced_cfg < 0) {
+    const char* f = getenv("DTG_GEMM_CFG");
+    g_forced_cfg = f ? atoi(f) : 0;
+  }
+  return g_forced_cfg;
+}
+void gemm_force_cfg(int cfg) { g_forced_cfg = cfg; }
+
+static bool launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B,
+                          long long ldb, int M, int N, int K, int split_k, int kps, const Epi& e, float* ws,
+                          hipStream_t st, const GemmBatch& bt) {
+#define DTG_CFG_CASE(n, ...)                                                                          \
+  case n:                                                                                            \
+    launch_exact<__VA_ARGS__>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt); \
+    return true;
+  switch (cfg) {
+    DTG_CFG_CASE(1, Cfg<128, 128, 1>)
+    DTG_CFG_CASE(2, Cfg<128, 128, 2>)
+    DTG_CFG_CASE(3, Cfg<128, 128, 3>)
+    DTG_CFG_CASE(4, Cfg<128, 128, 4>)
+    DTG_CFG_CASE(5, Cfg<256, 64, 2>)
+    DTG_CFG_CASE(6, Cfg<256, 64, 3>)
+    DTG_CFG_CASE(7, Cfg<256, 64, 4>)
+    DTG_CFG_CASE(8, Cfg<256, 128, 3, 8>)
+    DTG_CFG_CASE(9, Cfg<256, 128, 2, 8>)
+    DTG_CFG_CASE(10, Cfg<128, 256, 2, 8>)
+    DTG_CFG_CASE(11, Cfg<128, 256, 3, 8>)
+    DTG_CFG_CASE(12, Cfg<64, 256, 2>)
+    DTG_CFG_CASE(13, Cfg<64, 256, 3>)
+    default: return false;
+  }
+#undef DTG_CFG_CASE
+}
+
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
   if (N % 8 == 0 && split_k > 16) {
     const long long plane = (long long)M * N;
@@ -247,6 +293,13 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
+  if (const int fc = forced_cfg()) {
+    if (fc == 99 && bt.count == 1) {
+      gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
+      return;
+    }
+    if (launch_forced(fc, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt)) return;
+  }
   if (bt.count == 1 && use_8phase(M, N, K, split_k)) {
     gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
     return;

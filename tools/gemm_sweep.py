@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Tile-configuration sweep of the MFMA GEMM on the ResNet-50 / BERT shapes (gemm_force_cfg):
+one line per (shape, config) with time, TB/s and TFLOP/s; the fastest config per shape is marked.
+This is the data the heuristic in csrc/kernels/gemm.hip (gemm_bf16) is fitted to.
+
+    python tools/gemm_sweep.py [--json out.json] [--cfgs 0,1,2,...]
+Configs: 0 heuristic, 1-4 128x128 S=1..4, 5-7 256x64 S=2..4, 8 256x128x3 (8 waves),
+9 256x128x2 (8w), 10 128x256x2 (8w), 11 128x256x3 (8w), 12-13 64x256 S=2..3, 99 8-phase 256x256.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import dtg  # noqa: E402,F401
+from dtg.ops._native import lib  # noqa: E402
+
+NAMES = {0: "heur", 1: "128x128s1", 2: "128x128s2", 3: "128x128s3", 4: "128x128s4", 5: "256x64s2", 6: "256x64s3",
+         7: "256x64s4", 8: "256x128s3w8", 9: "256x128s2w8", 10: "128x256s2w8", 11: "128x256s3w8", 12: "64x256s2",
+         13: "64x256s3", 99: "8phase"}
+
+# (M, N, K, a_kc, b_kc, beta): the memory-bound and mid-size GEMMs of a ResNet-50 batch-256 step
+SHAPES = [
+    (802816, 64, 256, True, True, 0.0), (802816, 256, 64, True, True, 0.0), (802816, 256, 64, True, False, 1.0),
+    (802816, 64, 256, True, False, 0.0), (200704, 128, 512, True, True, 0.0), (200704, 512, 128, True, True, 0.0),
+    (200704, 512, 128, True, False, 1.0), (50176, 1024, 256, True, True, 0.0), (50176, 1024, 256, True, False, 1.0),
+    (50176, 256, 1024, True, True, 0.0), (12544, 2048, 512, True, True, 0.0), (12544, 512, 2048, True, True, 0.0),
+    (200704, 256, 512, True, True, 0.0), (802816, 128, 256, True, True, 0.0),
+    (16384, 768, 3072, True, True, 0.0), (16384, 3072, 768, True, True, 0.0), (16384, 2304, 768, True, True, 0.0),
+]
+
+
+def timeit(fn, iters=10, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default="")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,99")
+    a = ap.parse_args()
+    L = lib()
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    res = []
+    for (M, N, K, akc, bkc, beta) in SHAPES:
+        A = torch.randn((M, K) if akc else (K, M), device="cuda", dtype=torch.bfloat16)
+        B = torch.randn((N, K) if bkc else (K, N), device="cuda", dtype=torch.bfloat16)
+        C = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        ref = None
+        by = (A.numel() + B.numel()) * 2 + C.numel() * 2 * (2 if beta else 1)
+        fl = 2.0 * M * N * K
+        rows = []
+        for c in cfgs:
+            if c in (5, 6, 7) and N > 64 and N % 64:
+                continue
+            L.gemm_force_cfg(c)
+            out = torch.zeros_like(C)
+            L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, 1)
+            if ref is None:
+                ref = out.float()
+            err = ((out.float() - ref).norm() / (ref.norm() + 1e-9)).item()
+            us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, 1))
+            rows.append((c, us, err))
+        L.gemm_force_cfg(0)
+        best = min(r[1] for r in rows)
+        for c, us, err in rows:
+            mark = " *" if us == best else ""
+            print(f"{M:7d}x{N:5d}x{K:5d} {'KC' if akc else 'MC'}{'KC' if bkc else 'MC'} b={beta:.0f} "
+                  f"{NAMES[c]:12s} {us:8.1f} us {by / us / 1e6:5.2f} TB/s {fl / us / 1e6:6.1f} TF/s err={err:.1e}{mark}",
+                  flush=True)
+            res.append({"M": M, "N": N, "K": K, "akc": akc, "bkc": bkc, "beta": beta, "cfg": NAMES[c], "us": us,
+                        "err": err})
+        del A, B, C
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
