@@ -402,6 +402,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("softmax_xent", &softmax_xent);
   m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
+  m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });
   m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"), pybind11::arg("b_kc"),
         pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,

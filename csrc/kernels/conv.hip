@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "dtg/common.h"
+#include <stdlib.h>
 #include "dtg/gemm_epi.cuh"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
@@ -369,6 +370,26 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideC
 // ---------------------------------------------------------------------------------------------
 static bool conv_skinny(int n) { return n <= 64; }
 
+// LDS ring depth of the implicit-GEMM kernels: 1 (32-40 KB of LDS, ~4 workgroups per CU hide latency
+// across blocks) or 2 (64-80 KB, 2 per CU, DMA of the next K-step under the current one).
+// DTG_CONV_STAGES / conv_set_stages() select it per pass (fwd, dgrad, wgrad) for A/B runs.
+// Default (measured, profiles/r01_tiles): one stage, except fwd/dgrad grids shorter than 512
+// 128x128 tiles with a reduction of >= 2048 (the 7x7 / 512-channel layers), which keep the 2-deep ring.
+static int g_conv_stages[3] = {0, 0, 0};
+static int conv_stages(int which, long long M = 0, int N = 0, int Kred = 0) {
+  if (g_conv_stages[which] == 0) {
+    const char* f = getenv("DTG_CONV_STAGES");
+    g_conv_stages[which] = f ? (atoi(f) == 1 ? 1 : 2) : -1;
+  }
+  if (g_conv_stages[which] > 0) return g_conv_stages[which];
+  if (which == 2) return 1;
+  const long long tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  return (tiles < 512 && Kred >= 2048) ? 2 : 1;
+}
+void conv_set_stages(int which, int stages) {  // 0 restores the measured default
+  if (which >= 0 && which < 3) g_conv_stages[which] = stages == 1 ? 1 : (stages == 2 ? 2 : -1);
+}
+
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
   if (C % 64 || K % 64) return 0;
   if (which == 1 && stride * stride > kMaxClasses) return 0;  // one launch holds <= 9 residue classes
@@ -380,15 +401,14 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   const int M = N * G.P * G.Q;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
-  if (conv_skinny(K)) {
-    using CF = Cfg<256, 64, 2>;
+  auto run = [&](auto cf) {
+    using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
     conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn);
-  } else {
-    using CF = Cfg<128, 128, 2>;
-    const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn);
-  }
+  };
+  const bool s1 = conv_stages(0, M, K, R * S * C) == 1;
+  if (conv_skinny(K)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
+  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
 }
 
 static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
@@ -434,8 +454,14 @@ static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t
     return a.nr * a.ns > b.nr * b.ns;
   });
   const dim3 grid(max_tiles, nc);
-  if (skinny) conv_dgrad_s_kernel<Cfg<256, 64, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
-  else conv_dgrad_s_kernel<Cfg<128, 128, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+  const bool s1 = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s)) == 1;
+  if (skinny) {
+    if (s1) conv_dgrad_s_kernel<Cfg<256, 64, 1>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+    else conv_dgrad_s_kernel<Cfg<256, 64, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+  } else {
+    if (s1) conv_dgrad_s_kernel<Cfg<128, 128, 1>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+    else conv_dgrad_s_kernel<Cfg<128, 128, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
+  }
 }
 
 void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
@@ -444,15 +470,14 @@ void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int
   if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st);
   const int M = N * H * W;
   Epi e{dx, C, 1, 1.f, beta, nullptr, 0};
-  if (conv_skinny(C)) {
-    using CF = Cfg<256, 64, 2>;
+  auto run = [&](auto cf) {
+    using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
     conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn);
-  } else {
-    using CF = Cfg<128, 128, 2>;
-    const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn);
-  }
+  };
+  const bool s1 = conv_stages(1, M, C, R * S * K) == 1;
+  if (conv_skinny(C)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
+  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
 }
 
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
@@ -478,8 +503,9 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
     dim3 grid(tm * tn, split);
     conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
   };
-  if (K <= 64) run(Cfg<64, 256, 2>());  // 64 output channels: one 64-row tile, no wasted MFMA rows
-  else run(Cfg<128, 128, 2>());
+  const bool s1 = conv_stages(2) == 1;
+  if (K <= 64) s1 ? run(Cfg<64, 256, 1>()) : run(Cfg<64, 256, 2>());  // 64 output channels: one 64-row tile
+  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
   gemm_splitk_reduce(ws, split, K, No, e, st);
 }
 

@@ -196,7 +196,8 @@ static bool use_8phase(int M, int N, int K, int split_k) {
   // CU), so compare round utilisation, crediting the 8-phase kernel with its per-CU advantage, which
   // grows with K (measured, profiles/r01_gemm8: ~1.15x at K = 768 in a cold-cache training step, up
   // to ~2x at K >= 2048); it loses at K = 256 (prologue/epilogue dominated).
-  if (split_k != 1 || M < 256 || N < 256 || K < 512) return false;
+  // r01_tiles sweep: at K <= 3072 the single-stage 128x128 / 64x256 rings match or beat it
+  if (split_k != 1 || M < 256 || N < 256 || K < 4096) return false;
   const long long t8 = (long long)((M + 255) / 256) * ((N + 255) / 256);
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
   if (t8 < 48) return false;
@@ -266,6 +267,8 @@ static bool launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long lon
     DTG_CFG_CASE(11, Cfg<128, 256, 3, 8>)
     DTG_CFG_CASE(12, Cfg<64, 256, 2>)
     DTG_CFG_CASE(13, Cfg<64, 256, 3>)
+    DTG_CFG_CASE(14, Cfg<256, 64, 1>)
+    DTG_CFG_CASE(15, Cfg<64, 256, 1>)
     default: return false;
   }
 #undef DTG_CFG_CASE
@@ -304,11 +307,31 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
     return;
   }
-  if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else if (short_m(M, N))  // 64-row weight gradients (64-channel layers): no half-empty 128-row tiles
+  if (short_m(M, N)) {  // 64-row weight gradients (64-channel layers): no half-empty 128-row tiles
     launch_cfg<64, 256>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else if (use_big(M, N, kps, split_k, bt)) launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    return;
+  }
+  if (use_big(M, N, kps, split_k, bt)) {
+    launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    return;
+  }
+  // Tile width follows N so the streamed activation operand A is read as few times as possible:
+  // 256x64 for N <= 64, 128x128 for N = 128, 64x256 for N >= 256.  LDS ring depth: a single stage
+  // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
+  // (< 512 tiles) and K long enough (>= 2048) that in-block prefetch pays (profiles/r01_tiles).
+  const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * split_k * bt.count;
+  if (split_k > 1 || !a_kc) {  // split-K weight gradients: tile/ring choice measured flat (r01_tiles)
+    if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  } else if (tiles128 < 512 && kps >= 2048) {
+    launch_exact<Cfg<128, 128, 2>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  } else if (skinny(N)) {
+    launch_exact<Cfg<256, 64, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  } else if (N >= 256 && M >= 64) {
+    launch_exact<Cfg<64, 256, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  } else {
+    launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  }
 }
 
 }  // namespace dtg

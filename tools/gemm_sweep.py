@@ -21,7 +21,7 @@ from dtg.ops._native import lib  # noqa: E402
 
 NAMES = {0: "heur", 1: "128x128s1", 2: "128x128s2", 3: "128x128s3", 4: "128x128s4", 5: "256x64s2", 6: "256x64s3",
          7: "256x64s4", 8: "256x128s3w8", 9: "256x128s2w8", 10: "128x256s2w8", 11: "128x256s3w8", 12: "64x256s2",
-         13: "64x256s3", 99: "8phase"}
+         13: "64x256s3", 14: "256x64s1", 15: "64x256s1", 99: "8phase"}
 
 # (M, N, K, a_kc, b_kc, beta): the memory-bound and mid-size GEMMs of a ResNet-50 batch-256 step
 SHAPES = [
@@ -31,6 +31,10 @@ SHAPES = [
     (50176, 256, 1024, True, True, 0.0), (12544, 2048, 512, True, True, 0.0), (12544, 512, 2048, True, True, 0.0),
     (200704, 256, 512, True, True, 0.0), (802816, 128, 256, True, True, 0.0),
     (16384, 768, 3072, True, True, 0.0), (16384, 3072, 768, True, True, 0.0), (16384, 2304, 768, True, True, 0.0),
+    # weight gradients dW = dY^T X (both operands MN-contiguous, K = batch*H*W, auto split-K)
+    (64, 256, 802816, False, False, 1.0), (256, 64, 802816, False, False, 1.0), (128, 512, 200704, False, False, 1.0),
+    (512, 128, 200704, False, False, 1.0), (256, 1024, 50176, False, False, 1.0), (1024, 256, 50176, False, False, 1.0),
+    (2048, 512, 12544, False, False, 1.0),
 ]
 
 
@@ -50,29 +54,32 @@ def timeit(fn, iters=10, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="")
-    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,99")
+    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,99")
+    ap.add_argument("--shapes", default="", help="comma list of shape indices (default all)")
     a = ap.parse_args()
     L = lib()
     cfgs = [int(c) for c in a.cfgs.split(",")]
     res = []
-    for (M, N, K, akc, bkc, beta) in SHAPES:
+    idx = [int(i) for i in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
+    for (M, N, K, akc, bkc, beta) in [SHAPES[i] for i in idx]:
+        split = 0 if K >= 8192 else 1  # wgrad shapes: the binding's automatic split-K
         A = torch.randn((M, K) if akc else (K, M), device="cuda", dtype=torch.bfloat16)
         B = torch.randn((N, K) if bkc else (K, N), device="cuda", dtype=torch.bfloat16)
-        C = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+        C = torch.randn(M, N, device="cuda", dtype=torch.float32 if split == 0 else torch.bfloat16)
         ref = None
         by = (A.numel() + B.numel()) * 2 + C.numel() * 2 * (2 if beta else 1)
         fl = 2.0 * M * N * K
         rows = []
         for c in cfgs:
-            if c in (5, 6, 7) and N > 64 and N % 64:
+            if c in (5, 6, 7, 14) and N > 64 and N % 64:
                 continue
             L.gemm_force_cfg(c)
             out = torch.zeros_like(C)
-            L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, 1)
+            L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, split)
             if ref is None:
                 ref = out.float()
             err = ((out.float() - ref).norm() / (ref.norm() + 1e-9)).item()
-            us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, 1))
+            us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, split))
             rows.append((c, us, err))
         L.gemm_force_cfg(0)
         best = min(r[1] for r in rows)

@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--json", default="")
+    ap.add_argument("--conv-stages", default="", help="LDS ring depth of conv fwd,dgrad,wgrad, e.g. 1,1,2")
+    ap.add_argument("--gemm-cfg", type=int, default=0, help="force one GEMM tile config (gemm_sweep numbering)")
     a = ap.parse_args()
     import torch
     import dtg  # noqa: F401
@@ -92,6 +94,11 @@ def main():
     from dtg.ops._native import lib
 
     L = lib()
+    if a.conv_stages:
+        for i, v in enumerate(a.conv_stages.split(",")):
+            L.conv_set_stages(i, int(v))
+    if a.gemm_cfg:
+        L.gemm_force_cfg(a.gemm_cfg)
     dev = torch.device("cuda")
     records = []
     active = [False]
@@ -140,6 +147,13 @@ def main():
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0.record()
+    for _ in range(5):
+        step()
+    c1.record()
+    torch.cuda.synchronize()
+    clean_ms = c0.elapsed_time(c1) / 5
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     active[0] = True
     t0.record()
@@ -164,6 +178,7 @@ def main():
                      "lost_us": us - bound})
     rows.sort(key=lambda r: -r["lost_us"])
     covered = sum(r["us"] for r in rows)
+    print(f"uninstrumented step {clean_ms:.2f} ms (conv stages {a.conv_stages or 'default'}, gemm cfg {a.gemm_cfg})")
     print(f"step {total:.0f} us; instrumented ops {covered:.0f} us; roofline bound of those "
           f"{sum(r['bound_us'] for r in rows):.0f} us")
     print(f"{'op':52s} {'calls':>5s} {'us':>8s} {'TF/s':>7s} {'TB/s':>6s} {'eff':>5s} {'lost us':>8s}")
@@ -172,7 +187,7 @@ def main():
               f"{r['eff']:5.2f} {r['lost_us']:8.1f}")
     if a.json:
         with open(a.json, "w") as f:
-            json.dump({"step_us": total, "rows": rows}, f, indent=1)
+            json.dump({"step_us": total, "clean_ms": clean_ms, "rows": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
