@@ -356,6 +356,182 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   return dx;
 }
 
+// ---- BN statistics fused into the producing GEMM / conv (dtg/bn_epi.cuh) ----------------------
+Tensor bn_part(const Tensor& like, int64_t C) {
+  return at::zeros({(long long)dtg::kBnStatSlots * 2 * C}, like.options().dtype(at::kFloat));
+}
+
+dtg::BnEpi bn_bwd_epi(Tensor& part, const Tensor& x, const Tensor& mean, const Tensor& invstd, const Tensor& gamma,
+                      const Tensor& beta, long long M, int C) {
+  CHECK_IN(x);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.numel() == M * C, "BN input shape mismatch");
+  for (const Tensor* t : {&mean, &invstd, &gamma, &beta}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  dtg::BnEpi bn;
+  bn.part = part.data_ptr<float>();
+  bn.mode = 2;
+  bn.x = cbfp(x);
+  bn.mean = mean.data_ptr<float>();
+  bn.invstd = invstd.data_ptr<float>();
+  bn.gamma = gamma.data_ptr<float>();
+  bn.beta = beta.data_ptr<float>();
+  return bn;
+}
+
+// mode 1: out = A W^T (W [N,K]) + forward BN statistics of out.
+// mode 2: dp = (dY W) * relu'(bn(x)) (W [K,N]) + backward BN partials (x, mean, invstd, gamma, beta given).
+std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::optional<Tensor> x,
+                                   c10::optional<Tensor> mean, c10::optional<Tensor> invstd,
+                                   c10::optional<Tensor> gamma, c10::optional<Tensor> beta) {
+  CHECK_IN(A);
+  CHECK_DT(A, at::kBFloat16);
+  CHECK_CUDA(B);
+  CHECK_DT(B, at::kBFloat16);
+  TORCH_CHECK(mode == 1 || mode == 2, "mode in {1, 2}");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && B.stride(1) == 1, "2-D operands, contiguous rows");
+  const int M = (int)A.size(0), K = (int)A.size(1);
+  const int N = (int)(mode == 1 ? B.size(0) : B.size(1));
+  TORCH_CHECK((mode == 1 ? B.size(1) : B.size(0)) == K, "gemm_bn K mismatch");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0 && B.stride(0) % 8 == 0, "K, N and row strides must be multiples of 8");
+  TORCH_CHECK(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0, "16-byte alignment");
+  c10::DeviceGuard dg(A.device());
+  auto out = at::empty({M, N}, A.options());
+  auto part = bn_part(A, N);
+  dtg::BnEpi bn;
+  if (mode == 2) {
+    TORCH_CHECK(x && mean && invstd && gamma && beta, "mode 2 needs x, mean, invstd, gamma, beta");
+    bn = bn_bwd_epi(part, *x, *mean, *invstd, *gamma, *beta, M, N);
+  } else {
+    bn.part = part.data_ptr<float>();
+    bn.mode = 1;
+  }
+  dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(out), N, M, N, K, bn, cur_stream());
+  return {out, part};
+}
+
+std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int K = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(w.size(3) == C, "weight channels mismatch");
+  TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 0), "conv shape not supported by the HIP kernel");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty output");
+  TORCH_CHECK((long long)N * H * W * C < (1LL << 31) && (long long)N * P * Q * K < (1LL << 31), "tensor too large");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, P, Q, K}, x.options());
+  auto part = bn_part(x, K);
+  dtg::BnEpi bn;
+  bn.part = part.data_ptr<float>();
+  bn.mode = 1;
+  dtg::conv_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, C, K, R, S, stride, pad, cur_stream(), bn);
+  return {y, part};
+}
+
+// dp = dgrad(dy, w) * relu'(bn(x)) with backward BN partials; x is the BN input [N,H,W,C]
+std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
+                                         Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta) {
+  check_nhwc(dy, "dy");
+  check_nhwc(w, "w");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
+  const int R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(w.size(0) == K, "weight/dy channel mismatch");
+  TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 1), "dgrad shape not supported by the HIP kernel");
+  TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q, "dgrad geometry mismatch");
+  c10::DeviceGuard dg(dy.device());
+  auto dx = at::empty({N, H, W, C}, dy.options());
+  auto part = bn_part(dy, C);
+  dtg::BnEpi bn = bn_bwd_epi(part, x, mean, invstd, gamma, beta, (long long)N * H * W, C);
+  TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn),
+              "conv_dgrad_bn: geometry leaves rows unwritten (use conv_dgrad + bn_bwd)");
+  return {dx, part};
+}
+
+std::tuple<Tensor, Tensor, Tensor> bn_fwd_part(Tensor x, Tensor part, c10::optional<Tensor> res, Tensor gamma,
+                                               Tensor beta, Tensor rmean, Tensor rvar, double momentum, double eps,
+                                               bool relu) {
+  CHECK_IN(x);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2, "x must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  CHECK_IN(part);
+  CHECK_DT(part, at::kFloat);
+  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  const bool has_res = res.has_value() && res->defined();
+  if (has_res) {
+    CHECK_IN(*res);
+    CHECK_DT(*res, at::kBFloat16);
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt), ws = at::empty({2LL * C}, fopt);
+  dtg::bn_fwd_from_part(cbfp(x), has_res ? cbfp(*res) : nullptr, bfp(y), gamma.data_ptr<float>(),
+                        beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                        smean.data_ptr<float>(), sinv.data_ptr<float>(), part.data_ptr<float>(), ws.data_ptr<float>(),
+                        M, C, (float)momentum, (float)eps, relu, cur_stream());
+  return {y, smean, sinv};
+}
+
+std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp, Tensor x, Tensor part, Tensor gamma,
+                                                                       Tensor smean, Tensor sinv, bool want_dres,
+                                                                       c10::optional<Tensor> dgamma_acc,
+                                                                       c10::optional<Tensor> dbeta_acc) {
+  CHECK_IN(dp);
+  CHECK_IN(x);
+  CHECK_DT(dp, at::kBFloat16);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && dp.numel() == x.numel(), "dp/x must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  CHECK_IN(part);
+  CHECK_DT(part, at::kFloat);
+  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  for (const Tensor* t : {&gamma, &smean, &sinv}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto dx = at::empty_like(x);
+  c10::optional<Tensor> dres;
+  if (want_dres) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined() && dbeta_acc.has_value() && dbeta_acc->defined();
+  Tensor dgamma, dbeta;
+  if (acc) {
+    dgamma = *dgamma_acc;
+    dbeta = *dbeta_acc;
+    for (const Tensor* t : {&dgamma, &dbeta}) {
+      CHECK_IN(*t);
+      CHECK_DT(*t, at::kFloat);
+      TORCH_CHECK(t->numel() == C, "gradient accumulator size mismatch");
+    }
+  } else {
+    dgamma = at::empty({C}, fopt);
+    dbeta = at::empty({C}, fopt);
+  }
+  auto ws = at::empty({3LL * C}, fopt);
+  dtg::bn_bwd_from_part(cbfp(dp), cbfp(x), gamma.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
+                        part.data_ptr<float>(), bfp(dx), want_dres ? bfp(*dres) : nullptr, dgamma.data_ptr<float>(),
+                        dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, acc, cur_stream());
+  return {dx, dres, dgamma, dbeta};
+}
+
 // dw (+)= wgrad; dw is [K, R, S, C] contiguous, fp32 or bf16 (beta = 1 accumulates into a flat grad)
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad) {
   check_nhwc(dy, "dy");
@@ -388,6 +564,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("beta") = 0.0);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
+        pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
+        pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
+        pybind11::arg("beta") = pybind11::none());
+  m.def("conv_fwd_bn", &conv_fwd_bn);
+  m.def("conv_dgrad_bn", &conv_dgrad_bn);
+  m.def("bn_fwd_part", &bn_fwd_part);
+  m.def("bn_bwd_part", &bn_bwd_part);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);
   m.def("momentum_apply", &momentum_apply);

@@ -1,0 +1,97 @@
+// BatchNorm statistics fused into the MFMA GEMM / implicit-GEMM epilogue (see BnEpi in kernels.h).
+//
+// ResNet's BN layers read every conv output once more just to reduce it per channel (forward: sum,
+// sum of squares; backward: sum(dp), sum(dp*xhat)).  The epilogue already holds each output tile in
+// registers, so it reduces its tile column-wise on the way out and adds one partial per column into
+// a small slot buffer: the separate statistics pass (one full read of an M x C activation per BN)
+// disappears.  In backward the ReLU mask is recomputed from the BN input and the saved per-channel
+// statistics (gamma*xhat + beta > 0, the same fp32 expression the forward apply evaluates), so the
+// BN output need not be re-read, and the stored gradient is already masked: the dx pass then reads
+// dp and x only.
+//
+// Thread -> column mapping: epilogue_staged hands thread `tid` the 8-column group tid % (BN/8) in
+// every pass (NTH is a multiple of BN/8), so each thread accumulates 8 columns in registers over all
+// its rows; the block then reduces over the NTH/(BN/8) threads sharing a group through LDS.
+#pragma once
+#include "dtg/common.h"
+#include "dtg/kernels.h"
+#include "dtg/gemm_epi.cuh"
+#include "dtg/mfma_gemm.cuh"
+
+namespace dtg {
+namespace gemm {
+
+template <class C, int MODE, class ROWMAP>
+__device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+                                            const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
+  static_assert(MODE == 1 || MODE == 2, "BN epilogue mode");
+  constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
+  static_assert(C::NTH % CPR == 0, "fixed column group per thread");
+  static_assert(2 * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
+  const int tid = threadIdx.x, cg = tid % CPR, n0 = bn0 + cg * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float mu[8], is[8], sc[8], sf[8];
+  if constexpr (MODE == 2) {
+    if (n0 < N) {
+      float g[8], b[8];
+      load8_f32(bn.mean + n0, mu);
+      load8_f32(bn.invstd + n0, is);
+      load8_f32(bn.gamma + n0, g);
+      load8_f32(bn.beta + n0, b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sc[k] = g[k] * is[k];       // = bn_finalize's coef (scale)
+        sf[k] = b[k] - mu[k] * sc[k];  // = bn_finalize's coef (shift)
+      }
+    }
+  }
+  epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
+    const int row = rowmap(m);
+    if constexpr (MODE == 1) {
+      epi_store8(e, N, row, n, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float r = bf2f(f2bf(v[k]));  // statistics of what the apply pass will read
+        s[k] += r;
+        q[k] += r * r;
+      }
+    } else {
+      const long long off = (long long)row * e.ldc + n;
+      float xv[8];
+      load8_bf16(bn.x + off, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
+        v[k] = d;
+        s[k] += d;
+        q[k] += d * ((xv[k] - mu[k]) * is[k]);
+      }
+      store8_bf16((bf16_t*)e.C + off, v);
+    }
+  });
+  // epilogue_staged ended with a barrier: the LDS ring is free for the column reduction
+  lds_float* red = reinterpret_cast<lds_float*>(smem);
+  const int r = tid / CPR;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[r * C::BN + cg * 8 + k] = s[k];
+    red[(RW + r) * C::BN + cg * 8 + k] = q[k];
+  }
+  __syncthreads();
+  float* part = bn.part + (long long)(tile_id % kBnStatSlots) * 2 * N;
+  for (int c = tid; c < C::BN; c += C::NTH) {
+    if (bn0 + c < N) {
+      float ts = 0.f, tq = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < RW; ++j) {
+        ts += red[j * C::BN + c];
+        tq += red[(RW + j) * C::BN + c];
+      }
+      atomicAdd(part + bn0 + c, ts);
+      atomicAdd(part + N + bn0 + c, tq);
+    }
+  }
+}
+
+}  // namespace gemm
+}  // namespace dtg

@@ -23,8 +23,34 @@ void adam_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* m, f
 void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st);
 void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
 
+// ---- BatchNorm statistics fused into a GEMM / implicit-GEMM epilogue (dtg/bn_epi.cuh) ----------
+// mode 1 (forward): per output column c, sum and sum of squares of the stored (bf16) output.
+// mode 2 (backward through BN -> ReLU): the epilogue turns the GEMM result g (= dL/da, a = relu(bn(x)))
+//   into dp = g * [gamma*xhat + beta > 0] (stored instead of g) and accumulates sum(dp) and
+//   sum(dp * xhat), xhat = (x - mean) * invstd, x = the BN input (same layout as the output).
+// Partials land in part[kBnStatSlots][2][N] (zero-initialised fp32, atomically accumulated; tile t
+// adds into slot t % kBnStatSlots) and are reduced by the BN finalize kernel.
+constexpr int kBnStatSlots = 32;
+struct BnEpi {
+  float* part = nullptr;
+  int mode = 0;
+  const bf16_t* x = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+};
+
 // ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
 long long bn_workspace_floats(long long M, int C);
+// finish a forward BN from fused-epilogue statistics: finalize (coef = ws[0:2C]) + apply
+void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                      float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
+                      int C, float momentum, float eps, int relu, hipStream_t st);
+// finish a backward BN from mode-2 partials: dx = a*dp + bx*x + c0 (ws: 3C floats), dres = dp if given
+void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
+                      const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
+                      int C, int accum, hipStream_t st);
 void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                   float* rmean, float* rvar, float* smean, float* sinv, float* ws, long long M, int C,
                   float momentum, float eps, int relu, hipStream_t st);
@@ -54,6 +80,10 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st, const GemmBatch& batch = GemmBatch(), void* aux = nullptr,
                int aux_mode = 0);
+// C[M,N] (bf16, row stride ldc) = A * op(B) with BN statistics in the epilogue (bn.mode 1: B is [N,K]
+// (forward); bn.mode 2: B is [K,N] (dgrad)).  A is [M,K] K-contiguous.  No split-K.
+void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
+                  int N, int K, const BnEpi& bn, hipStream_t st);
 
 // ---- transformer blocks (transformer.hip) ------------------------------------------------------
 int ln_max_hidden();
@@ -103,9 +133,11 @@ void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, 
 // which: 0 fwd, 1 dgrad, 2 wgrad.  Strided dgrad runs one dense launch per residue class of dx.
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
-              int stride, int pad, hipStream_t st);
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-                int stride, int pad, float beta, hipStream_t st);
+              int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
+// returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad
+// with residue classes no tap reaches)
+int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
+               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi());
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad);
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,

@@ -349,16 +349,8 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
     default: { constexpr int T = 64; __VA_ARGS__; } break; \
   }
 
-void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
-                  float* rmean, float* rvar, float* smean, float* sinv, float* ws, long long M, int C,
-                  float momentum, float eps, int relu, hipStream_t st) {
-  const BnGeom g = bn_geom(M, C);
-  float* part = ws;
-  float* coef = ws + (long long)g.nchunk * 2 * C;
-  dim3 grid(g.nchunk, g.gy);
-  DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
-                                                    momentum, eps, coef, nullptr, nullptr);
+static void bn_apply_launch(const BnGeom& g, const bf16_t* x, const bf16_t* res, bf16_t* y, const float* coef,
+                            long long M, int C, int relu, hipStream_t st) {
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
@@ -370,6 +362,29 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
       else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
     }
   });
+}
+
+void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                  float* rmean, float* rvar, float* smean, float* sinv, float* ws, long long M, int C,
+                  float momentum, float eps, int relu, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  float* part = ws;
+  float* coef = ws + (long long)g.nchunk * 2 * C;
+  dim3 grid(g.nchunk, g.gy);
+  DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
+                                                    momentum, eps, coef, nullptr, nullptr);
+  bn_apply_launch(g, x, res, y, coef, M, C, relu, st);
+}
+
+// Statistics already reduced by a GEMM / conv epilogue (kBnStatSlots partials): finalize + apply.
+void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
+                      float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
+                      int C, float momentum, float eps, int relu, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+                                                    sinv, momentum, eps, ws, nullptr, nullptr);
+  bn_apply_launch(g, x, res, y, ws, M, C, relu, st);
 }
 
 // Inference: coefficients from running statistics (tiny launch) then the same apply pass.
@@ -427,6 +442,22 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
       if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
       else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
     }
+  });
+}
+
+// Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
+void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
+                      const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
+                      int C, int accum, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+                                                    nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
+                                                    0.f, ws, dgamma, dbeta);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
+  DTG_TPR_SWITCH(g.tpr, {
+    if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+    else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
   });
 }
 

@@ -21,6 +21,7 @@
 #include "dtg/gemm_epi.cuh"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
+#include "dtg/bn_epi.cuh"
 
 namespace dtg {
 using namespace gemm;
@@ -264,9 +265,9 @@ struct DgradSB {
 };
 
 // ---------------------------------------------------------------------------------------------
-template <class CF>
+template <class CF, int BNMODE = 0>
 __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
-                                                         const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+                                                         const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -284,12 +285,16 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
   mainloop_st<CF, true, true>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
                               [&](lds_char* tl, int k0) { stage_kc<CF::BN>(sb, tl, bn0, k0, wave, lane); }, smem, 0,
                               Kd, acc);
+  if constexpr (BNMODE != 0) {
+    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.K, e, bn, t, [](int m) { return m; });
+    return;
+  }
   epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.K, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.K, m, n, v); });
 }
 
-template <class CF>
+template <class CF, int BNMODE = 0>
 __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
-                                                           const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+                                                           const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -306,6 +311,10 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
                                [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
+  if constexpr (BNMODE != 0) {
+    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.C, e, bn, t, [](int m) { return m; });
+    return;
+  }
   epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.C, m, n, v); });
 }
 
@@ -336,10 +345,11 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   });
 }
 
-template <class CF>
+template <class CF, int BNMODE = 0>
 __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideClasses SC,
                                                              const bf16_t* __restrict__ dy,
-                                                             const bf16_t* __restrict__ w, Epi e, int tiles_n) {
+                                                             const bf16_t* __restrict__ w, Epi e, int tiles_n,
+                                                             BnEpi bn) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const StrideClass S = SC.c[blockIdx.y];
@@ -358,13 +368,17 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideC
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
                                [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
-  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) {
+  auto rowmap = [&](int m) {
     uint32_t nn, ij, ii, jj;
     S.fHWc.divmod((uint32_t)m, nn, ij);
     S.fWc.divmod(ij, ii, jj);
-    const int row = ((int)nn * G.H + G.stride * (int)ii + S.ph) * G.W + G.stride * (int)jj + S.pw;
-    epi_store8(e, G.C, row, n, v);
-  });
+    return ((int)nn * G.H + G.stride * (int)ii + S.ph) * G.W + G.stride * (int)jj + S.pw;
+  };
+  if constexpr (BNMODE != 0) {  // slot index spread over the residue classes too
+    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.C, e, bn, t + (int)blockIdx.y * 7, rowmap);
+    return;
+  }
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.C, rowmap(m), n, v); });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -397,22 +411,23 @@ int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
 }
 
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
-              int stride, int pad, hipStream_t st) {
+              int stride, int pad, hipStream_t st, const BnEpi& bn) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   const int M = N * G.P * G.Q;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn);
+    if (bn.mode == 1) conv_fwd_kernel<CF, 1><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
+    else conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
   };
   const bool s1 = conv_stages(0, M, K, R * S * C) == 1;
   if (conv_skinny(K)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
   else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
 }
 
-static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
-                               hipStream_t st) {
+static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
+                              hipStream_t st, const BnEpi& bn) {
   const int s = G.stride;
   bool empty = false;
   for (int ph = 0; ph < s; ++ph)
@@ -420,6 +435,7 @@ static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t
       const int r0 = ((ph + G.pad) % s + s) % s, s0 = ((pw + G.pad) % s + s) % s;
       if (r0 >= G.R || s0 >= G.S || ph >= G.H || pw >= G.W) empty = true;
     }
+  if (empty && bn.mode != 0) return 0;  // rows no launch writes would be missing from the statistics
   if (empty && beta == 0.f) {  // residue classes no tap reaches are zero
     DTG_HIP_CHECK(hipMemsetAsync(dx, 0, (size_t)G.N * G.H * G.W * G.C * sizeof(bf16_t), st));
     beta = 1.f;
@@ -448,36 +464,39 @@ static void conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t
       max_tiles = S.tiles > max_tiles ? S.tiles : max_tiles;
       SC.c[nc++] = S;
     }
-  if (nc == 0) return;
+  if (nc == 0) return bn.mode == 0;
   // heaviest residue class (most taps) first: blocks dispatch in y-major order
   std::stable_sort(SC.c, SC.c + nc, [](const StrideClass& a, const StrideClass& b) {
     return a.nr * a.ns > b.nr * b.ns;
   });
   const dim3 grid(max_tiles, nc);
   const bool s1 = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s)) == 1;
-  if (skinny) {
-    if (s1) conv_dgrad_s_kernel<Cfg<256, 64, 1>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
-    else conv_dgrad_s_kernel<Cfg<256, 64, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
-  } else {
-    if (s1) conv_dgrad_s_kernel<Cfg<128, 128, 1>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
-    else conv_dgrad_s_kernel<Cfg<128, 128, 2>><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn);
-  }
+  auto run = [&](auto cf) {
+    using CF = decltype(cf);
+    if (bn.mode == 2) conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
+    else conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
+  };
+  if (skinny) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
+  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  return 1;
 }
 
-void conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-                int stride, int pad, float beta, hipStream_t st) {
+int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
+               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
-  if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st);
+  if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st, bn);
   const int M = N * H * W;
   Epi e{dx, C, 1, 1.f, beta, nullptr, 0};
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn);
+    if (bn.mode == 2) conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
+    else conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
   };
   const bool s1 = conv_stages(1, M, C, R * S * K) == 1;
   if (conv_skinny(C)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
   else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  return 1;
 }
 
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {

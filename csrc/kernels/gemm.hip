@@ -10,15 +10,17 @@
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
 #include "dtg/gemm_epi.cuh"
+#include "dtg/bn_epi.cuh"
 #include <stdlib.h>
 #include <type_traits>
 
 namespace dtg {
 using namespace gemm;
 
-template <class CF, bool AKC, bool BKC, class SA, class SB>
+template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0>
 __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
-                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt) {
+                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
+                                                     BnEpi bn) {
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   if (bt.count > 1) {  // batched problem z: offset the operands (element strides)
@@ -42,6 +44,10 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
+  if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
+    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, N, e, bn, t, [](int m) { return m; });
+    return;
+  }
   if (split_k > 1) {
     float* slab = ws + (long long)split * M * N;
     const bool vec = (N & 3) == 0;
@@ -154,7 +160,7 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   dim3 grid(tiles_m * tiles_n, split_k, bt.count);
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws, bt);
+                     kps, e, ws, bt, BnEpi());
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 
@@ -332,6 +338,46 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   } else {
     launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   }
+}
+
+// ---- BN-statistics epilogue (gemm_bf16_bn) ---------------------------------------------------------
+template <class CF, int MODE, bool GUARD>
+static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                      const Epi& e, const BnEpi& bn, hipStream_t st) {
+  using SA = DenseKC<GUARD>;
+  using SB = std::conditional_t<MODE == 1, DenseKC<GUARD>, DenseMC<GUARD>>;
+  SA sa{A, lda, M, K};
+  SB sb{B, ldb, N, K};
+  const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
+  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE>), dim3(tiles_m * tiles_n, 1, 1), dim3(CF::NTH), 0,
+                     st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
+}
+
+template <class CF, int MODE>
+static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                          const Epi& e, const BnEpi& bn, hipStream_t st) {
+  const bool full = (M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0);
+  if (full) launch_bn<CF, MODE, false>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else launch_bn<CF, MODE, true>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
+template <int MODE>
+static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                             const Epi& e, const BnEpi& bn, hipStream_t st) {
+  // same tile choice as gemm_bf16's heuristic
+  const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles128 < 512 && K >= 2048) launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (skinny(N)) launch_bn_cfg<Cfg<256, 64, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (N >= 256 && M >= 64) launch_bn_cfg<Cfg<64, 256, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
+void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
+                  int N, int K, const BnEpi& bn, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  Epi e{C, ldc, 1, 1.f, 0.f, nullptr, 0};
+  if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
 }  // namespace dtg

@@ -14,7 +14,15 @@ Everything runs on dtg's HIP kernels on [rows, channels] views of NHWC activatio
             buckets are notified through parallel/grad_sink.
 Strided dgrads (3x3/s2 and the 1x1/s2 projection) run dtg's residue-class dgrad kernel; the
 projection's accumulates (beta = 1) straight into the conv1 dgrad output.
+
+BN statistics are fused into the producing GEMM/conv epilogue (csrc/include/dtg/bn_epi.cuh):
+forward, every conv output's per-channel sum / sum of squares; backward, the dgrads feeding BN2 and
+BN1 emit the relu-masked gradient plus sum(dp) and sum(dp*xhat).  Each BN then costs finalize +
+one elementwise pass instead of a reduction pass + finalize + elementwise pass.  DTG_BN_FUSE=0
+restores the separate statistics kernels (A/B runs).
 """
+import os
+
 import torch
 
 from ..ops._native import lib
@@ -38,6 +46,9 @@ def _krsc(w):  # channels_last [K, C, R, S] -> contiguous [K, R, S, C] view
     return w.permute(0, 2, 3, 1)
 
 
+_FUSE = os.environ.get("DTG_BN_FUSE", "1") != "0"
+
+
 def _gacc(p):
     """The buffer a parameter's gradient is accumulated into (its flat view, or a fresh one)."""
     if grad_sink.enabled(p):
@@ -57,26 +68,49 @@ class _BottleneckFn(torch.autograd.Function):
         p_, q_ = (h + 2 - 3) // st + 1, (w + 2 - 3) // st + 1
         b1, b2, b3 = blk.c1.bn, blk.c2.bn, blk.c3.bn
         w1, w2, w3 = blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight
-        y1 = gemm(x2, True, _mat(w1), True)
-        a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
-                                    b1.eps, True)
-        y2 = L.conv_fwd(a1.view(n, h, w, width), _krsc(w2), st, 1).view(-1, width)
-        a2, m2, i2 = L.bn_fwd_train(y2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.momentum,
-                                    b2.eps, True)
-        y3 = gemm(a2, True, _mat(w3), True)
+        if _FUSE:
+            y1, p1 = L.gemm_bn(x2, _mat(w1), 1)
+            a1, m1, i1 = L.bn_fwd_part(y1, p1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var,
+                                       b1.momentum, b1.eps, True)
+            y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1)
+            y2 = y2.view(-1, width)
+            a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
+                                       b2.momentum, b2.eps, True)
+            y3, p3 = L.gemm_bn(a2, _mat(w3), 1)
+        else:
+            y1 = gemm(x2, True, _mat(w1), True)
+            a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
+                                        b1.eps, True)
+            y2 = L.conv_fwd(a1.view(n, h, w, width), _krsc(w2), st, 1).view(-1, width)
+            a2, m2, i2 = L.bn_fwd_train(y2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.momentum,
+                                        b2.eps, True)
+            y3 = gemm(a2, True, _mat(w3), True)
         yd = md = idd = None
         if blk.down is not None:
             bd, wd = blk.down.bn, blk.down.conv.weight
-            if st == 1:
-                yd = gemm(x2, True, _mat(wd), True)
+            if _FUSE:
+                if st == 1:
+                    yd, pd = L.gemm_bn(x2, _mat(wd), 1)
+                else:
+                    yd, pd = L.conv_fwd_bn(x2.view(n, h, w, c), _krsc(wd), st, 0)
+                    yd = yd.view(-1, cout)
+                idn, md, idd = L.bn_fwd_part(yd, pd, None, bd.weight, bd.bias, bd.running_mean, bd.running_var,
+                                             bd.momentum, bd.eps, False)
             else:
-                yd = L.conv_fwd(x2.view(n, h, w, c), _krsc(wd), st, 0).view(-1, cout)
-            idn, md, idd = L.bn_fwd_train(yd, None, bd.weight, bd.bias, bd.running_mean, bd.running_var, bd.momentum,
-                                          bd.eps, False)
+                if st == 1:
+                    yd = gemm(x2, True, _mat(wd), True)
+                else:
+                    yd = L.conv_fwd(x2.view(n, h, w, c), _krsc(wd), st, 0).view(-1, cout)
+                idn, md, idd = L.bn_fwd_train(yd, None, bd.weight, bd.bias, bd.running_mean, bd.running_var,
+                                              bd.momentum, bd.eps, False)
         else:
             idn = x2
-        out, m3, i3 = L.bn_fwd_train(y3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.momentum,
-                                     b3.eps, True)
+        if _FUSE:
+            out, m3, i3 = L.bn_fwd_part(y3, p3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var,
+                                        b3.momentum, b3.eps, True)
+        else:
+            out, m3, i3 = L.bn_fwd_train(y3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.momentum,
+                                         b3.eps, True)
         ctx.blk = blk
         ctx.geom = (n, c, h, w, st, width, cout, p_, q_)
         ctx.save_for_backward(x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3,
@@ -100,16 +134,29 @@ class _BottleneckFn(torch.autograd.Function):
         do = _rows(dout)
         # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
         dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)], g[id(b3.bias)])
-        # conv3 (1x1)
-        da2 = gemm(dy3, True, _mat(w3), False)
+        # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
+        if _FUSE:
+            dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias)
+        else:
+            da2 = gemm(dy3, True, _mat(w3), False)
         gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
         # BN2 + conv2 (3x3)
-        dy2, _, _, _ = L.bn_bwd(da2, a2, y2, b2.weight, m2, i2, True, False, g[id(b2.weight)], g[id(b2.bias)])
+        if _FUSE:
+            dy2 = L.bn_bwd_part(dp2, y2, q2, b2.weight, m2, i2, False, g[id(b2.weight)], g[id(b2.bias)])[0]
+        else:
+            dy2 = L.bn_bwd(da2, a2, y2, b2.weight, m2, i2, True, False, g[id(b2.weight)], g[id(b2.bias)])[0]
         dy2_4 = dy2.view(n, p_, q_, width)
-        da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
+        if _FUSE:
+            dp1, q1 = L.conv_dgrad_bn(dy2_4, _krsc(w2).contiguous(), h, w, st, 1, y1, m1, i1, b1.weight, b1.bias)
+            dp1 = dp1.view(-1, width)
+        else:
+            da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
         L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
         # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
-        dy1, _, _, _ = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])
+        if _FUSE:
+            dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
+        else:
+            dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         dx_done = False
         if blk.down is not None:
             yd, md, idd = sv[13:16]

@@ -1,0 +1,135 @@
+"""BatchNorm statistics fused into the GEMM / implicit-GEMM epilogues (csrc/include/dtg/bn_epi.cuh)
+against plain fp32 PyTorch references of the same math."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dtg  # noqa: F401
+from dtg.ops._native import lib
+
+pytestmark = pytest.mark.gpu
+SLOTS = 32
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _bn_stats(part, n):
+    p = part.view(SLOTS, 2, n).sum(0)
+    return p[0], p[1]
+
+
+def _bwd_ref(g, x, mean, inv, gamma, beta):
+    """dp = g * [relu(bn(x)) > 0], sum(dp), sum(dp * xhat) in fp32."""
+    sc = gamma * inv
+    sf = beta - mean * sc
+    xf = x.float()
+    dp = torch.where(xf * sc + sf > 0, g, torch.zeros_like(g))
+    xhat = (xf - mean) * inv
+    return dp, dp.sum(0), (dp * xhat).sum(0)
+
+
+def _chan(n, dev, g):
+    mean = (torch.randn(n, generator=g) * 0.3).to(dev)
+    inv = (torch.rand(n, generator=g) + 0.5).to(dev)
+    gamma = (torch.rand(n, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(n, generator=g) * 0.2).to(dev)
+    return mean, inv, gamma, beta
+
+
+# (M, N, K): skinny (256x64), 128x128, 64x256 and the 2-stage short-grid tiles, plus ragged M
+@pytest.mark.parametrize("M,N,K", [(4096, 64, 256), (2048, 128, 512), (1024, 256, 64), (640, 512, 2048),
+                                   (1000, 192, 128)])
+def test_gemm_bn_fwd_stats(M, N, K):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    out, part = lib().gemm_bn(a, w, 1)
+    ref = a.float() @ w.float().t()
+    assert _rel(out, ref) < 1e-2
+    s, q = _bn_stats(part, N)
+    of = out.float()
+    assert _rel(s, of.sum(0)) < 1e-3
+    assert _rel(q, (of * of).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 64, 256), (2048, 128, 512), (1024, 256, 128), (1000, 192, 64)])
+def test_gemm_bn_bwd_stats(M, N, K):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    dy = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(K, N, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)  # stored [K, N] (dgrad)
+    x = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    mean, inv, gamma, beta = _chan(N, dev, g)
+    dp, part = lib().gemm_bn(dy, w, 2, x, mean, inv, gamma, beta)
+    gref = dy.float() @ w.float()
+    dpr, sr, qr = _bwd_ref(gref, x, mean, inv, gamma, beta)
+    assert _rel(dp, dpr) < 1e-2
+    s, q = _bn_stats(part, N)
+    assert _rel(s, sr) < 1e-2
+    assert _rel(q, qr) < 1e-2
+
+
+@pytest.mark.parametrize("C,K,H,R,st,pad", [(64, 64, 14, 3, 1, 1), (128, 128, 14, 3, 2, 1), (64, 256, 8, 1, 1, 0),
+                                            (256, 512, 7, 3, 1, 1)])
+def test_conv_bn_fwd_and_dgrad_stats(C, K, H, R, st, pad):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(2)
+    N = 4
+    x = torch.randn(N, C, H, H, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, R, R, generator=g).mul_((C * R * R) ** -0.5).to(dev, torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last)
+    L = lib()
+    y, part = L.conv_fwd_bn(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), st, pad)
+    yr = F.conv2d(x.float(), w.float(), stride=st, padding=pad).permute(0, 2, 3, 1)
+    assert _rel(y, yr) < 1e-2
+    yf = y.float().reshape(-1, K)
+    s, q = _bn_stats(part, K)
+    assert _rel(s, yf.sum(0)) < 1e-3 and _rel(q, (yf * yf).sum(0)) < 1e-3
+    # dgrad through BN(x)->relu of the conv INPUT x (channels C)
+    dy = torch.randn(yr.shape, generator=g).to(dev, torch.bfloat16).contiguous()
+    mean, inv, gamma, beta = _chan(C, dev, g)
+    xin = x.permute(0, 2, 3, 1).contiguous()
+    dp, part = L.conv_dgrad_bn(dy, w.permute(0, 2, 3, 1).contiguous(), H, H, st, pad, xin.view(-1, C), mean, inv,
+                               gamma, beta)
+    gref = torch.nn.grad.conv2d_input((N, C, H, H), w.float(), dy.permute(0, 3, 1, 2).float(), stride=st,
+                                      padding=pad).permute(0, 2, 3, 1).reshape(-1, C)
+    dpr, sr, qr = _bwd_ref(gref, xin.view(-1, C), mean, inv, gamma, beta)
+    assert _rel(dp.view(-1, C), dpr) < 1e-2
+    s, q = _bn_stats(part, C)
+    assert _rel(s, sr) < 1e-2 and _rel(q, qr) < 1e-2
+
+
+@pytest.mark.parametrize("res", [False, True])
+def test_bn_part_matches_unfused(res):
+    """bn_fwd_part / bn_bwd_part (statistics from an epilogue) equal bn_fwd_train / bn_bwd."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    M, K, N = 3136, 128, 256
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    L = lib()
+    y, part = L.gemm_bn(a, w, 1)
+    gamma = (torch.rand(N, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(N, generator=g) * 0.1).to(dev)
+    r = torch.randn(M, N, generator=g).to(dev, torch.bfloat16) if res else None
+    rm0, rv0 = torch.zeros(N, device=dev), torch.ones(N, device=dev)
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    o0, m0, i0 = L.bn_fwd_train(y, r, gamma, beta, rm0, rv0, 0.1, 1e-5, True)
+    o1, m1, i1 = L.bn_fwd_part(y, part, r, gamma, beta, rm1, rv1, 0.1, 1e-5, True)
+    assert _rel(m1, m0) < 1e-4 and _rel(i1, i0) < 1e-4
+    assert _rel(rm1, rm0) < 1e-4 and _rel(rv1, rv0) < 1e-4
+    assert _rel(o1, o0) < 1e-2
+    # backward: reference bn_bwd on the unmasked gradient vs bn_bwd_part on (masked dp, reduced here)
+    do = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    dx0, _, dg0, db0 = L.bn_bwd(do, o0, y, gamma, m0, i0, True, False, None, None)
+    dp = torch.where(o0 > 0, do, torch.zeros_like(do))
+    xhat = (y.float() - m0) * i0
+    pr = torch.zeros(SLOTS, 2, N, device=dev)
+    pr[0, 0] = dp.float().sum(0)
+    pr[0, 1] = (dp.float() * xhat).sum(0)
+    dx1, _, dg1, db1 = L.bn_bwd_part(dp, y, pr.view(-1), gamma, m0, i0, False, None, None)
+    assert _rel(dg1, dg0) < 1e-3 and _rel(db1, db0) < 1e-3
+    assert _rel(dx1, dx0) < 1e-2

@@ -32,9 +32,13 @@ def test_resnet_tiny_loss_decreases():
 
 @pytest.mark.parametrize("cin,width,stride", [(64, 64, 1), (256, 64, 1), (256, 128, 2), (512, 128, 1)])
 @pytest.mark.parametrize("flat", [False, True])
-def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat):
-    """The hand-written bottleneck backward equals the layer-by-layer autograd path."""
+@pytest.mark.parametrize("bn_fuse", [True, False])
+def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, monkeypatch):
+    """The hand-written bottleneck backward (with and without BN statistics fused into the conv
+    epilogues) equals the layer-by-layer autograd path."""
     from dtg.models.resnet import Bottleneck
+    from dtg.models import resnet_fused
+    monkeypatch.setattr(resnet_fused, "_FUSE", bn_fuse)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     blocks = []

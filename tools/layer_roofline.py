@@ -75,7 +75,36 @@ def _bn_bwd_cost(args, kw):
             2 * (_nb(dy) + _nb(y) + _nb(x)) + _nb(dy) * (2 if want_dres else 1))
 
 
-COSTS = {"gemm": _gemm_cost, "conv_fwd": _conv_fwd_cost, "conv_dgrad": _conv_dgrad_cost,
+def _gemm_bn_cost(args, kw):
+    A, B, mode = args[:3]
+    M, K = A.shape
+    N = B.shape[0] if mode == 1 else B.shape[1]
+    by = _nb(A) + _nb(B) + M * N * 2 * (1 if mode == 1 else 2)  # mode 2 also reads the BN input
+    return f"gemm_bn{mode} {M}x{N}x{K}", 2.0 * M * N * K, by
+
+
+def _conv_fwd_bn_cost(args, kw):
+    lab, fl, by = _conv_fwd_cost(args, kw)
+    return lab.replace("conv_fwd", "conv_fwd_bn"), fl, by
+
+
+def _conv_dgrad_bn_cost(args, kw):
+    lab, fl, by = _conv_dgrad_cost(args[:6], {})
+    return lab.replace("conv_dgrad", "conv_dgrad_bn"), fl, by + _nb(args[6])
+
+
+def _bn_fwd_part_cost(args, kw):
+    x, res = args[0], args[2]
+    return f"bn_fwd_part {tuple(x.shape)}{' +res' if res is not None else ''}", 0.0, 2 * _nb(x) + _nb(res)
+
+
+def _bn_bwd_part_cost(args, kw):
+    dp, x = args[:2]
+    return f"bn_bwd_part {tuple(dp.shape)}", 0.0, 3 * _nb(dp)
+
+
+COSTS = {"gemm_bn": _gemm_bn_cost, "conv_fwd_bn": _conv_fwd_bn_cost, "conv_dgrad_bn": _conv_dgrad_bn_cost,
+         "bn_fwd_part": _bn_fwd_part_cost, "bn_bwd_part": _bn_bwd_part_cost, "gemm": _gemm_cost, "conv_fwd": _conv_fwd_cost, "conv_dgrad": _conv_dgrad_cost,
          "conv_wgrad": _conv_wgrad_cost, "bn_fwd_train": _bn_fwd_cost, "bn_bwd": _bn_bwd_cost}
 
 
