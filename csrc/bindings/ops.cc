@@ -384,14 +384,17 @@ dtg::BnEpi bn_bwd_epi(Tensor& part, const Tensor& x, const Tensor& mean, const T
 
 // mode 1: out = A W^T (W [N,K]) + forward BN statistics of out.
 // mode 2: dp = (dY W) * relu'(bn(x)) (W [K,N]) + backward BN partials (x, mean, invstd, gamma, beta given).
+// mode 3: dp = [mask > 0] * (dY W + beta*out) written into `out` (beta = 1 when out is given), partials
+//         with xhat from x (the BN input of the layer whose relu output `mask` is).
 std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::optional<Tensor> x,
                                    c10::optional<Tensor> mean, c10::optional<Tensor> invstd,
-                                   c10::optional<Tensor> gamma, c10::optional<Tensor> beta) {
+                                   c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
+                                   c10::optional<Tensor> mask, c10::optional<Tensor> out) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
   CHECK_DT(B, at::kBFloat16);
-  TORCH_CHECK(mode == 1 || mode == 2, "mode in {1, 2}");
+  TORCH_CHECK(mode >= 1 && mode <= 3, "mode in {1, 2, 3}");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && B.stride(1) == 1, "2-D operands, contiguous rows");
   const int M = (int)A.size(0), K = (int)A.size(1);
   const int N = (int)(mode == 1 ? B.size(0) : B.size(1));
@@ -399,18 +402,37 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0 && B.stride(0) % 8 == 0, "K, N and row strides must be multiples of 8");
   TORCH_CHECK(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0, "16-byte alignment");
   c10::DeviceGuard dg(A.device());
-  auto out = at::empty({M, N}, A.options());
+  Tensor o;
+  float bt = 0.f;
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(mode == 3, "accumulating into `out` is mode 3 only");
+    o = *out;
+    CHECK_IN(o);
+    CHECK_DT(o, at::kBFloat16);
+    TORCH_CHECK(o.numel() == (long long)M * N, "out shape mismatch");
+    bt = 1.f;
+  } else {
+    o = at::empty({M, N}, A.options());
+  }
   auto part = bn_part(A, N);
   dtg::BnEpi bn;
-  if (mode == 2) {
-    TORCH_CHECK(x && mean && invstd && gamma && beta, "mode 2 needs x, mean, invstd, gamma, beta");
+  if (mode >= 2) {
+    TORCH_CHECK(x && mean && invstd && gamma && beta, "modes 2/3 need x, mean, invstd, gamma, beta");
     bn = bn_bwd_epi(part, *x, *mean, *invstd, *gamma, *beta, M, N);
+    if (mode == 3) {
+      TORCH_CHECK(mask.has_value() && mask->defined(), "mode 3 needs the mask tensor");
+      CHECK_IN(*mask);
+      CHECK_DT(*mask, at::kBFloat16);
+      TORCH_CHECK(mask->numel() == (long long)M * N, "mask shape mismatch");
+      bn.mode = 3;
+      bn.mask = cbfp(*mask);
+    }
   } else {
     bn.part = part.data_ptr<float>();
     bn.mode = 1;
   }
-  dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(out), N, M, N, K, bn, cur_stream());
-  return {out, part};
+  dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(o), N, M, N, K, bt, bn, cur_stream());
+  return {o, part};
 }
 
 std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad) {
@@ -567,7 +589,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
-        pybind11::arg("beta") = pybind11::none());
+        pybind11::arg("beta") = pybind11::none(), pybind11::arg("mask") = pybind11::none(),
+        pybind11::arg("out") = pybind11::none());
   m.def("conv_fwd_bn", &conv_fwd_bn);
   m.def("conv_dgrad_bn", &conv_dgrad_bn);
   m.def("bn_fwd_part", &bn_fwd_part);

@@ -24,14 +24,14 @@ namespace gemm {
 template <class C, int MODE, class ROWMAP>
 __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                             const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
-  static_assert(MODE == 1 || MODE == 2, "BN epilogue mode");
+  static_assert(MODE >= 1 && MODE <= 3, "BN epilogue mode");
   constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
   static_assert(C::NTH % CPR == 0, "fixed column group per thread");
   static_assert(2 * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
   const int tid = threadIdx.x, cg = tid % CPR, n0 = bn0 + cg * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8], is[8], sc[8], sf[8];
-  if constexpr (MODE == 2) {
+  if constexpr (MODE >= 2) {
     if (n0 < N) {
       float g[8], b[8];
       load8_f32(bn.mean + n0, mu);
@@ -55,13 +55,27 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         s[k] += r;
         q[k] += r * r;
       }
-    } else {
+    } else if constexpr (MODE == 2) {
       const long long off = (long long)row * e.ldc + n;
       float xv[8];
       load8_bf16(bn.x + off, xv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
+        v[k] = d;
+        s[k] += d;
+        q[k] += d * ((xv[k] - mu[k]) * is[k]);
+      }
+      store8_bf16((bf16_t*)e.C + off, v);
+    } else {
+      const long long off = (long long)row * e.ldc + n;
+      float xv[8], mk[8], old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      load8_bf16(bn.x + off, xv);
+      load8_bf16(bn.mask + off, mk);
+      if (e.beta != 0.f) load8_bf16((const bf16_t*)e.C + off, old);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
         v[k] = d;
         s[k] += d;
         q[k] += d * ((xv[k] - mu[k]) * is[k]);

@@ -28,6 +28,9 @@ void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
 // mode 2 (backward through BN -> ReLU): the epilogue turns the GEMM result g (= dL/da, a = relu(bn(x)))
 //   into dp = g * [gamma*xhat + beta > 0] (stored instead of g) and accumulates sum(dp) and
 //   sum(dp * xhat), xhat = (x - mean) * invstd, x = the BN input (same layout as the output).
+// mode 3 (backward through BN -> +residual -> ReLU, computed by the NEXT layer's dgrad): like mode 2, but
+//   the relu mask is (mask > 0) for a given tensor (the block output) and the epilogue may accumulate
+//   (beta) into C first: dp = [mask > 0] * (alpha*acc + beta*C).
 // Partials land in part[kBnStatSlots][2][N] (zero-initialised fp32, atomically accumulated; tile t
 // adds into slot t % kBnStatSlots) and are reduced by the BN finalize kernel.
 constexpr int kBnStatSlots = 32;
@@ -39,6 +42,7 @@ struct BnEpi {
   const float* invstd = nullptr;
   const float* gamma = nullptr;
   const float* beta = nullptr;
+  const bf16_t* mask = nullptr;  // mode 3
 };
 
 // ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
@@ -80,10 +84,10 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st, const GemmBatch& batch = GemmBatch(), void* aux = nullptr,
                int aux_mode = 0);
-// C[M,N] (bf16, row stride ldc) = A * op(B) with BN statistics in the epilogue (bn.mode 1: B is [N,K]
-// (forward); bn.mode 2: B is [K,N] (dgrad)).  A is [M,K] K-contiguous.  No split-K.
+// C[M,N] (bf16, row stride ldc) = A * op(B) (+ beta*C in mode 3) with BN statistics in the epilogue
+// (bn.mode 1: B is [N,K] (forward); bn.mode 2/3: B is [K,N] (dgrad)).  A is [M,K] K-contiguous.
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
-                  int N, int K, const BnEpi& bn, hipStream_t st);
+                  int N, int K, float beta, const BnEpi& bn, hipStream_t st);
 
 // ---- transformer blocks (transformer.hip) ------------------------------------------------------
 int ln_max_hidden();

@@ -373,11 +373,12 @@ static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, lo
 }
 
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
-                  int N, int K, const BnEpi& bn, hipStream_t st) {
+                  int N, int K, float beta, const BnEpi& bn, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
-  Epi e{C, ldc, 1, 1.f, 0.f, nullptr, 0};
+  Epi e{C, ldc, 1, 1.f, bn.mode == 3 ? beta : 0.f, nullptr, 0};
   if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
 }  // namespace dtg

@@ -20,6 +20,14 @@ forward, every conv output's per-channel sum / sum of squares; backward, the dgr
 BN1 emit the relu-masked gradient plus sum(dp) and sum(dp*xhat).  Each BN then costs finalize +
 one elementwise pass instead of a reduction pass + finalize + elementwise pass.  DTG_BN_FUSE=0
 restores the separate statistics kernels (A/B runs).
+
+BN3 of block i (relu(bn3(y3) + identity) = the block output = block i+1's input) is reduced one
+block LATER: block i+1's last dgrad GEMM, the final writer of dL/d out_i, applies block i's relu
+mask (out_i > 0, i.e. its own saved input) and reduces block i's BN3 statistics in its epilogue
+(mode 3).  The two blocks meet through a _Bn3Link attached to the output tensor.  Block i uses the
+partials only if the gradient it receives is that very buffer (so nothing else was summed into it
+by autograd); otherwise it falls back to the full BN backward, which re-applies the (idempotent)
+mask.
 """
 import os
 
@@ -47,6 +55,16 @@ def _krsc(w):  # channels_last [K, C, R, S] -> contiguous [K, R, S, C] view
 
 
 _FUSE = os.environ.get("DTG_BN_FUSE", "1") != "0"
+_LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction (needs _FUSE)
+
+
+class _Bn3Link:
+    """Block i's BN3 tensors, filled with the mode-3 partials by block i+1's backward."""
+    __slots__ = ("y3", "m3", "i3", "gamma", "beta", "part", "dp")
+
+    def __init__(self, y3, m3, i3, gamma, beta):
+        self.y3, self.m3, self.i3, self.gamma, self.beta = y3, m3, i3, gamma, beta
+        self.part = self.dp = None
 
 
 def _gacc(p):
@@ -58,7 +76,7 @@ def _gacc(p):
 
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, blk, *params):
+    def forward(ctx, x, blk, link_in, holder, *params):
         L = lib()
         n, c, h, w = x.shape
         st = blk.c2.conv.stride
@@ -112,6 +130,9 @@ class _BottleneckFn(torch.autograd.Function):
             out, m3, i3 = L.bn_fwd_train(y3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.momentum,
                                          b3.eps, True)
         ctx.blk = blk
+        ctx.link_in = link_in if (_FUSE and _LINK) else None
+        ctx.link_out = _Bn3Link(y3, m3, i3, b3.weight, b3.bias) if (_FUSE and _LINK) else None
+        holder.append(ctx.link_out)
         ctx.geom = (n, c, h, w, st, width, cout, p_, q_)
         ctx.save_for_backward(x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3,
                               *((yd, md, idd) if yd is not None else ()))
@@ -133,7 +154,17 @@ class _BottleneckFn(torch.autograd.Function):
         g = {id(p): a for p, (a, _) in zip(params, accs)}
         do = _rows(dout)
         # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
-        dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)], g[id(b3.bias)])
+        lk = ctx.link_out
+        if (lk is not None and lk.part is not None and do.data_ptr() == lk.dp.data_ptr()
+                and do.shape == lk.dp.shape):
+            # block i+1 already masked dL/d out (do is dp) and reduced this BN's statistics
+            dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
+            dres = do  # our own buffer (pointer-checked above): dx accumulates into it in place
+        else:
+            dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)],
+                                       g[id(b3.bias)])
+        if lk is not None:
+            lk.part = lk.dp = None
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
         if _FUSE:
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias)
@@ -158,6 +189,10 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         dx_done = False
+        lk_in = ctx.link_in
+        ctx.link_in = None
+        if lk_in is not None and lk_in.y3.shape != x2.shape:
+            lk_in = None
         if blk.down is not None:
             yd, md, idd = sv[13:16]
             bd, wd = blk.down.bn, blk.down.conv.weight
@@ -166,6 +201,10 @@ class _BottleneckFn(torch.autograd.Function):
             if st == 1:
                 dx2 = gemm(dyd, True, _mat(wd), False)
                 gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
+            elif lk_in is not None:  # projection dgrad first, so the conv1 dgrad GEMM is the last writer
+                dx2 = L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0).view(-1, c)
+                L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
+                             st, 0)
             else:
                 dx2 = gemm(dy1, True, _mat(w1), False)
                 L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0, out=dx2.view(n, h, w, c),
@@ -176,7 +215,12 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dx2 = dres
         if not dx_done:
-            gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
+            if lk_in is not None:  # mode 3: finish the previous block's BN3 reduction in this epilogue
+                _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
+                                    mask=x2, out=dx2)
+                lk_in.part, lk_in.dp = part, dx2
+            else:
+                gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
         gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
         grads = []
         for p, (a, direct) in zip(params, accs):
@@ -185,7 +229,7 @@ class _BottleneckFn(torch.autograd.Function):
                 grads.append(None)
             else:
                 grads.append(a.to(p.dtype))
-        return (dx2.view(n, h, w, c).permute(0, 3, 1, 2), None, *grads)
+        return (dx2.view(n, h, w, c).permute(0, 3, 1, 2), None, None, None, *grads)
 
 
 def fused_ok(blk, x):
@@ -199,4 +243,8 @@ def bottleneck(blk, x):
               blk.c2.bn.bias, blk.c3.conv.weight, blk.c3.bn.weight, blk.c3.bn.bias]
     if blk.down is not None:
         params += [blk.down.conv.weight, blk.down.bn.weight, blk.down.bn.bias]
-    return _BottleneckFn.apply(x, blk, *params)
+    holder = []
+    y = _BottleneckFn.apply(x, blk, getattr(x, "_dtg_bn3", None), holder, *params)
+    if holder and holder[0] is not None:
+        y._dtg_bn3 = holder[0]
+    return y

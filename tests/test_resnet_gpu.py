@@ -76,6 +76,44 @@ def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, m
         assert torch.allclose(ba, bb, rtol=1e-3, atol=1e-4)
 
 
+def test_bn3_link_chain_matches_unlinked(monkeypatch):
+    """Three chained blocks (projection, identity, strided projection).  With the BN3 link each block's
+    BN3 statistics are reduced by the NEXT block's last dgrad epilogue (mode 3); without it, by the
+    block's own reduction pass.  Both runs share the same forward bit for bit (the link only changes
+    backward), so their gradients must agree to summation-order noise.  (Against the layer-wise
+    reference a 3-block chain differs by a few % through ReLU-mask flips of near-zero activations,
+    which is why the per-block test above is the fused-vs-layerwise check.)"""
+    from dtg.models.resnet import Bottleneck
+    from dtg.models import resnet_fused
+    monkeypatch.setattr(resnet_fused, "_FUSE", True)
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x0 = torch.randn(4, 64, 16, 16, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = None
+    outs, grads = [], []
+    for link in (False, True):
+        monkeypatch.setattr(resnet_fused, "_LINK", link)
+        torch.manual_seed(0)
+        bl = torch.nn.Sequential(Bottleneck(64, 64, 1), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2))
+        bl = bl.to(dev).to(memory_format=torch.channels_last)
+        for b in bl:
+            for bn in (b.c1.bn, b.c2.bn, b.c3.bn):
+                bn.weight.data.uniform_(0.5, 1.5)
+        bl.train()
+        FlatParams(bl)
+        x = x0.clone().requires_grad_()
+        y = bl(x)
+        if gy is None:
+            gy = torch.randn(y.shape, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y.backward(gy)
+        outs.append(y.float())
+        grads.append([x.grad.float()] + [p.grad.float().clone() for p in bl.parameters()])
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    assert rel(outs[1], outs[0]) == 0.0
+    errs = [rel(ga, gb) for ga, gb in zip(grads[1], grads[0])]
+    assert max(errs) < 1e-2, errs
+
+
 def test_resnet50_step_matches_reference_direction():
     """One ResNet-50 step on a small batch: finite loss, grads flow into the flat buffer."""
     torch.manual_seed(0)
