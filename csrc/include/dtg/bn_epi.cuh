@@ -48,7 +48,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
     const int row = rowmap(m);
     if constexpr (MODE == 1) {
-      epi_store8(e, N, row, n, v);
+      epi_store8_fast(e, row, n, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float r = bf2f(f2bf(v[k]));  // statistics of what the apply pass will read

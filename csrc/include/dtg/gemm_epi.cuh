@@ -84,6 +84,24 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
   }
 }
 
+// Fast path of epi_store8 for the common case: bf16 output, 8 full aligned columns, no bias /
+// activation / aux; C = alpha*acc (+ beta*C).  The generic version's per-group runtime switches cost
+// more VALU/SALU than the data movement in the memory-bound GEMMs (issue-bound epilogue, see
+// profiles/r01_pmc).
+__device__ __forceinline__ void epi_store8_fast(const Epi& e, int m, int n, float (&v)[8]) {
+  bf16_t* p = (bf16_t*)e.C + (long long)m * e.ldc + n;
+  if (e.beta != 0.f) {
+    float old[8];
+    load8_bf16(p, old);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], e.alpha, e.beta * old[k]);
+  } else if (e.alpha != 1.f) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+  }
+  store8_bf16(p, v);
+}
+
 // 256x256 8-wave 8-phase GEMM (gemm8.hip); same operand conventions as gemm_bf16, no batching
 void gemm8_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, const Epi& e,
                 int M, int N, int K, int split_k, int kps, float* ws, hipStream_t st);

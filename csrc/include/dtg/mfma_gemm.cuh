@@ -79,6 +79,7 @@ __device__ __forceinline__ int mc_swz(int k) {
 // KC: matrix stored [rows][ld] with k contiguous
 template <bool GUARD>
 struct DenseKC {
+  static constexpr bool kGuard = GUARD;
   const bf16_t* p;
   long long ld;
   int rows, K;
@@ -91,6 +92,7 @@ struct DenseKC {
 // MC: matrix stored [K][ld] with the row/col (M or N) index contiguous
 template <bool GUARD>
 struct DenseMC {
+  static constexpr bool kGuard = GUARD;
   const bf16_t* p;
   long long ld;
   int cols, K;
@@ -298,7 +300,7 @@ struct FastDiv {
 // Stages the block's fp32 accumulators through LDS (EPI_ROWS rows at a time) so that every
 // global store is a coalesced 16-byte vector; OP(row, col0, float (&v)[8]) finishes 8 consecutive
 // columns (bias, residual/beta, activation, dtype) and stores them.
-template <class C, class OP>
+template <class C, class OP, bool FULL = false>
 __device__ __forceinline__ void epilogue_staged(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                                 const OP& op) {
   constexpr int LD = C::BN + 4;  // fp32 row pitch (pad breaks bank aliasing of the column writes)
@@ -330,7 +332,7 @@ __device__ __forceinline__ void epilogue_staged(lds_char* smem, f32x4 (&acc)[4][
     for (int idx = tid; idx < R * CPR; idx += C::NTH) {
       const int rr = idx / CPR, cg = idx % CPR;
       const int m = bm0 + prow0 + rr, n = bn0 + cg * 8;
-      if (m < M && n < N) {
+      if (FULL || (m < M && n < N)) {
         float v[8];
         const lds_float* s = st + rr * LD + cg * 8;
 #pragma unroll

@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
     epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.K, e, bn, t, [](int m) { return m; });
     return;
   }
-  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.K, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.K, m, n, v); });
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.K, [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); });
 }
 
 template <class CF, int BNMODE = 0>
@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
     epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.C, e, bn, t, [](int m) { return m; });
     return;
   }
-  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.C, m, n, v); });
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); });
 }
 
 template <class CF>
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideC
     epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.C, e, bn, t + (int)blockIdx.y * 7, rowmap);
     return;
   }
-  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8(e, G.C, rowmap(m), n, v); });
+  epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.C, [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, rowmap(m), n, v); });
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -17,7 +17,7 @@
 namespace dtg {
 using namespace gemm;
 
-template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0>
+template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false>
 __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
                                                      BnEpi bn) {
@@ -59,7 +59,12 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
     });
     return;
   }
-  epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
+  if constexpr (FAST) {  // bf16, aligned, no bias/act/aux (fast_epi() checked): no per-group switches
+    auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); };
+    epilogue_staged<CF, decltype(op), !SA::kGuard && !SB::kGuard>(smem, acc, bm0, bn0, M, N, op);
+  } else {
+    epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
+  }
 }
 
 // Split-K reduction: a thread owns 8 consecutive outputs and sums their split_k partials; the
@@ -150,6 +155,12 @@ int gemm_pick_split(int M, int N, int K) {
   return s;
 }
 
+// epilogue specialisation: bf16 output, 16-B aligned 8-column groups, no bias / activation / aux
+static bool fast_epi(const Epi& e, int N) {
+  return e.c_bf16 && !e.bias && e.act == 0 && e.aux_mode == 0 && (e.ldc % 8) == 0 && (N % 8) == 0 &&
+         ((uintptr_t)e.C % 16) == 0;
+}
+
 template <class CF, bool AK, bool BK_, bool GUARD>
 static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
                    int kps, const Epi& e, float* ws, hipStream_t st, const GemmBatch& bt) {
@@ -159,8 +170,16 @@ static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   dim3 grid(tiles_m * tiles_n, split_k, bt.count);
+  if constexpr (AK) {  // (K-contiguous A = forward / dgrad GEMMs; weight gradients go through split-K)
+    if (split_k == 1 && fast_epi(e, N) && (bt.count == 1 || ((bt.sc_b | bt.sc_h) & 7) == 0)) {
+      hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB, 0, true>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K,
+                         tiles_n, split_k, kps, e, ws, bt, BnEpi());
+      if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
+      return;
+    }
+  }
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws, bt, BnEpi());
+                       kps, e, ws, bt, BnEpi());
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 
