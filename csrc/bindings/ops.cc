@@ -357,8 +357,21 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
 }
 
 // ---- BN statistics fused into the producing GEMM / conv (dtg/bn_epi.cuh) ----------------------
-Tensor bn_part(const Tensor& like, int64_t C) {
-  return at::zeros({(long long)dtg::kBnStatSlots * 2 * C}, like.options().dtype(at::kFloat));
+// Statistics slots.  pooled: a buffer from a per-device ring of zeroed buffers which the consuming
+// finalize (bn_*_part) zeroes again after reading -- no fill kernel per BN.  The caller must consume
+// (or zero) every pooled buffer before kPartRing more are handed out; the fused ResNet bottleneck
+// does (its producer -> consumer distance is at most 2).  Unpooled: a fresh zeroed tensor.
+constexpr int kPartRing = 16;
+constexpr long long kPartCap = (long long)dtg::kBnStatSlots * 2 * 2048;
+Tensor bn_part(const Tensor& like, int64_t C, bool pooled = false) {
+  if (!pooled || C > 2048) return at::zeros({(long long)dtg::kBnStatSlots * 2 * C}, like.options().dtype(at::kFloat));
+  static Tensor* ring = new Tensor[64];  // per device; leaked on purpose (no teardown-order issues)
+  static int next[64] = {0};
+  const int dev = like.get_device();
+  TORCH_CHECK(dev >= 0 && dev < 64, "device index");
+  if (!ring[dev].defined()) ring[dev] = at::zeros({kPartRing * kPartCap}, like.options().dtype(at::kFloat));
+  const int i = next[dev]++ % kPartRing;
+  return ring[dev].narrow(0, i * kPartCap, (long long)dtg::kBnStatSlots * 2 * C);
 }
 
 dtg::BnEpi bn_bwd_epi(Tensor& part, const Tensor& x, const Tensor& mean, const Tensor& invstd, const Tensor& gamma,
@@ -389,7 +402,7 @@ dtg::BnEpi bn_bwd_epi(Tensor& part, const Tensor& x, const Tensor& mean, const T
 std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::optional<Tensor> x,
                                    c10::optional<Tensor> mean, c10::optional<Tensor> invstd,
                                    c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
-                                   c10::optional<Tensor> mask, c10::optional<Tensor> out) {
+                                   c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
@@ -414,7 +427,7 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   } else {
     o = at::empty({M, N}, A.options());
   }
-  auto part = bn_part(A, N);
+  auto part = bn_part(A, N, pooled);
   dtg::BnEpi bn;
   if (mode >= 2) {
     TORCH_CHECK(x && mean && invstd && gamma && beta, "modes 2/3 need x, mean, invstd, gamma, beta");
@@ -435,7 +448,7 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   return {o, part};
 }
 
-std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad) {
+std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad, bool pooled) {
   check_nhwc(x, "x");
   check_nhwc(w, "w");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
@@ -447,7 +460,7 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   TORCH_CHECK((long long)N * H * W * C < (1LL << 31) && (long long)N * P * Q * K < (1LL << 31), "tensor too large");
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
-  auto part = bn_part(x, K);
+  auto part = bn_part(x, K, pooled);
   dtg::BnEpi bn;
   bn.part = part.data_ptr<float>();
   bn.mode = 1;
@@ -457,7 +470,8 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
 
 // dp = dgrad(dy, w) * relu'(bn(x)) with backward BN partials; x is the BN input [N,H,W,C]
 std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
-                                         Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta) {
+                                         Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta,
+                                         bool pooled) {
   check_nhwc(dy, "dy");
   check_nhwc(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -467,7 +481,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t
   TORCH_CHECK((H + 2 * pad - R) / stride + 1 == P && (W + 2 * pad - S) / stride + 1 == Q, "dgrad geometry mismatch");
   c10::DeviceGuard dg(dy.device());
   auto dx = at::empty({N, H, W, C}, dy.options());
-  auto part = bn_part(dy, C);
+  auto part = bn_part(dy, C, pooled);
   dtg::BnEpi bn = bn_bwd_epi(part, x, mean, invstd, gamma, beta, (long long)N * H * W, C);
   TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn),
               "conv_dgrad_bn: geometry leaves rows unwritten (use conv_dgrad + bn_bwd)");
@@ -506,6 +520,43 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_part(Tensor x, Tensor part, c10::optio
                         smean.data_ptr<float>(), sinv.data_ptr<float>(), part.data_ptr<float>(), ws.data_ptr<float>(),
                         M, C, (float)momentum, (float)eps, relu, cur_stream());
   return {y, smean, sinv};
+}
+
+// out = relu(bn(x) + bn2(r)), both from epilogue partials -> (out, mean, invstd, mean2, invstd2)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> bn_fwd2_part(Tensor x, Tensor part, Tensor gamma, Tensor beta,
+                                                                Tensor rmean, Tensor rvar, Tensor r, Tensor part2,
+                                                                Tensor gamma2, Tensor beta2, Tensor rmean2,
+                                                                Tensor rvar2, double momentum, double eps) {
+  CHECK_IN(x);
+  CHECK_IN(r);
+  CHECK_DT(x, at::kBFloat16);
+  CHECK_DT(r, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && r.sizes() == x.sizes(), "x/r must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  for (const Tensor* t : {&part, &part2}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  }
+  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar, &gamma2, &beta2, &rmean2, &rvar2}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto m1 = at::empty({C}, fopt), i1 = at::empty({C}, fopt), m2 = at::empty({C}, fopt), i2 = at::empty({C}, fopt);
+  auto ws = at::empty({4LL * C}, fopt);
+  dtg::bn_fwd2_from_part(cbfp(x), cbfp(r), bfp(y), part.data_ptr<float>(), part2.data_ptr<float>(),
+                         gamma.data_ptr<float>(), beta.data_ptr<float>(), rmean.data_ptr<float>(),
+                         rvar.data_ptr<float>(), m1.data_ptr<float>(), i1.data_ptr<float>(), gamma2.data_ptr<float>(),
+                         beta2.data_ptr<float>(), rmean2.data_ptr<float>(), rvar2.data_ptr<float>(),
+                         m2.data_ptr<float>(), i2.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)momentum,
+                         (float)eps, cur_stream());
+  return {y, m1, i1, m2, i2};
 }
 
 std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp, Tensor x, Tensor part, Tensor gamma,
@@ -590,9 +641,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
         pybind11::arg("beta") = pybind11::none(), pybind11::arg("mask") = pybind11::none(),
-        pybind11::arg("out") = pybind11::none());
-  m.def("conv_fwd_bn", &conv_fwd_bn);
-  m.def("conv_dgrad_bn", &conv_dgrad_bn);
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false);
+  m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),
+        pybind11::arg("pad"), pybind11::arg("pooled") = false);
+  m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),
+        pybind11::arg("W"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("x"), pybind11::arg("mean"),
+        pybind11::arg("invstd"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("pooled") = false);
+  m.def("bn_fwd2_part", &bn_fwd2_part);
   m.def("bn_fwd_part", &bn_fwd_part);
   m.def("bn_bwd_part", &bn_bwd_part);
   m.doc() = "dtg gfx950 HIP kernels";

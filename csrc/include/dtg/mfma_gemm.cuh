@@ -44,12 +44,15 @@ typedef __attribute__((address_space(3))) float lds_float;
 constexpr int BK = 64;
 constexpr int NT = 256;
 
-template <int BM_, int BN_, int STAGES_ = 2, int NW_ = 4>
+// BK_ = K depth of one ring stage: 64 (128-B LDS rows) or 32 (64-B rows: half the LDS per stage, so a
+// deep ring still leaves room for several workgroups per CU).
+template <int BM_, int BN_, int STAGES_ = 2, int NW_ = 4, int BK_ = 64>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_, NW = NW_, NTH = NW_ * 64;
+  static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_, NW = NW_, NTH = NW_ * 64, BK = BK_;
   static constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == NW, "one 64x64 sub-tile per wave");
   static_assert(STAGES >= 1 && STAGES <= 5, "ring depth");
+  static_assert(BK == 64 || BK == 32, "stage depth");
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int LDS_BYTES = STAGES * STAGE_BYTES;
@@ -106,28 +109,43 @@ struct DenseMC {
 };
 
 // ---- staging ---------------------------------------------------------------------------------
-// KC tile: ROWS x 64 k (128 B rows); a wave-instruction covers 8 rows; NW waves share the tile
-template <int ROWS, class Src, int NW = 4>
+// KC tile: ROWS x 64 k (128 B rows, chunk XOR (row & 7)); a wave-instruction covers 8 rows; NW waves
+// share the tile.  BKT = 32: ROWS x 32 k (64 B rows, 4 chunks, chunk XOR ((row >> 2) & 3): the 16 rows one
+// ds_read_b128 lane group touches then hit 16 distinct 16-B slots); a wave-instruction covers 16 rows.
+template <int ROWS, class Src, int NW = 4, int BKT = 64>
 __device__ __forceinline__ void stage_kc(const Src& src, lds_char* lds_tile, int row0, int k0, int wave, int lane) {
-  constexpr int PER_WAVE = ROWS / (8 * NW);
-  static_assert(PER_WAVE >= 1, "tile too small for the wave count");
+  if constexpr (BKT == 64) {
+    constexpr int PER_WAVE = ROWS / (8 * NW);
+    static_assert(PER_WAVE >= 1, "tile too small for the wave count");
 #pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    const int r0 = (wave * PER_WAVE + i) * 8;
-    const int r = r0 + (lane >> 3);
-    const int cl = lane & 7;           // linear chunk position in LDS
-    const int c = cl ^ (r & 7);        // source chunk that belongs there
-    const void* g = src.chunk(row0 + r, k0 + c * 8);
-    __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_tile + r0 * 128), 16, 0, 0);
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int r0 = (wave * PER_WAVE + i) * 8;
+      const int r = r0 + (lane >> 3);
+      const int cl = lane & 7;           // linear chunk position in LDS
+      const int c = cl ^ (r & 7);        // source chunk that belongs there
+      const void* g = src.chunk(row0 + r, k0 + c * 8);
+      __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_tile + r0 * 128), 16, 0, 0);
+    }
+  } else {
+    constexpr int PER_WAVE = ROWS / (16 * NW);
+    static_assert(PER_WAVE >= 1, "tile too small for the wave count");
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int r0 = (wave * PER_WAVE + i) * 16;
+      const int r = r0 + (lane >> 2);
+      const int c = (lane & 3) ^ ((r >> 2) & 3);
+      const void* g = src.chunk(row0 + r, k0 + c * 8);
+      __builtin_amdgcn_global_load_lds(g, (lds_void*)(lds_tile + r0 * 64), 16, 0, 0);
+    }
   }
 }
 
-// MC tile: 64 k-rows x ROWS cols (2*ROWS B rows); a wave-instruction covers 512/ROWS k-rows
-template <int ROWS, class Src, int NW = 4>
+// MC tile: BKT k-rows x ROWS cols (2*ROWS B rows); a wave-instruction covers 512/ROWS k-rows
+template <int ROWS, class Src, int NW = 4, int BKT = 64>
 __device__ __forceinline__ void stage_mc(const Src& src, lds_char* lds_tile, int col0, int k0, int wave, int lane) {
   constexpr int CH = ROWS / 8;          // 16-B chunks per k-row
   constexpr int KPI = 64 / CH;          // k-rows per wave-instruction
-  constexpr int PER_WAVE = 64 / KPI / NW;
+  constexpr int PER_WAVE = BKT / KPI / NW;
   static_assert(PER_WAVE >= 1, "tile too small for the wave count");
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
@@ -142,10 +160,16 @@ __device__ __forceinline__ void stage_mc(const Src& src, lds_char* lds_tile, int
 
 // ---- fragment reads (one 16x32 operand fragment for mfma_f32_16x16x32_bf16) --------------------
 // lane l holds X[r0 + (l&15)][ks*32 + 8*(l>>4) + j], j = 0..7
+template <int BKT = 64>
 __device__ __forceinline__ v8bf frag_kc(const lds_char* lds_tile, int r0, int ks, int lane) {
   const int r = r0 + (lane & 15);
-  const int c = ks * 4 + (lane >> 4);
-  return *reinterpret_cast<const lds_v8bf*>(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
+  if constexpr (BKT == 64) {
+    const int c = ks * 4 + (lane >> 4);
+    return *reinterpret_cast<const lds_v8bf*>(lds_tile + r * 128 + ((c ^ (r & 7)) << 4));
+  } else {
+    const int c = lane >> 4;
+    return *reinterpret_cast<const lds_v8bf*>(lds_tile + r * 64 + ((c ^ ((r >> 2) & 3)) << 4));
+  }
 }
 
 template <int ROWS>
@@ -163,32 +187,32 @@ __device__ __forceinline__ v8bf frag_mc(const lds_char* lds_tile, int r0, int ks
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int BKT = 64>
 __device__ __forceinline__ v8bf frag(const lds_char* t, int r0, int ks, int lane) {
-  if constexpr (KC) return frag_kc(t, r0, ks, lane);
+  if constexpr (KC) return frag_kc<BKT>(t, r0, ks, lane);
   else return frag_mc<ROWS>(t, r0, ks, lane);
 }
 
-template <bool KC, int ROWS, class Src, int NW = 4>
+template <bool KC, int ROWS, class Src, int NW = 4, int BKT = 64>
 __device__ __forceinline__ void stage(const Src& s, lds_char* t, int rc0, int k0, int wave, int lane) {
-  if constexpr (KC) stage_kc<ROWS, Src, NW>(s, t, rc0, k0, wave, lane);
-  else stage_mc<ROWS, Src, NW>(s, t, rc0, k0, wave, lane);
+  if constexpr (KC) stage_kc<ROWS, Src, NW, BKT>(s, t, rc0, k0, wave, lane);
+  else stage_mc<ROWS, Src, NW, BKT>(s, t, rc0, k0, wave, lane);
 }
 
 // LDS-DMA instructions one wave issues to stage one K-step of a ROWS-wide operand
-template <int ROWS, int NW>
-constexpr int stage_loads() { return (ROWS * 64 * 2) / (1024 * NW); }
+template <int ROWS, int NW, int BKT = 64>
+constexpr int stage_loads() { return (ROWS * BKT * 2) / (1024 * NW); }
 
 template <class C, bool AKC, bool BKC>
 __device__ __forceinline__ void compute_tile(const lds_char* At, const lds_char* Bt, int wm, int wn, int lane,
                                              f32x4 (&acc)[4][4]) {
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < C::BK / 32; ++ks) {
     v8bf a[4], b[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = frag<AKC, C::BM>(At, wm * 64 + i * 16, ks, lane);
+    for (int i = 0; i < 4; ++i) a[i] = frag<AKC, C::BM, C::BK>(At, wm * 64 + i * 16, ks, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = frag<BKC, C::BN>(Bt, wn * 64 + j * 16, ks, lane);
+    for (int j = 0; j < 4; ++j) b[j] = frag<BKC, C::BN, C::BK>(Bt, wn * 64 + j * 16, ks, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -206,6 +230,7 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
+  constexpr int BK = C::BK;
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk <= 0) return;
   if constexpr (C::STAGES == 1) {
@@ -226,7 +251,7 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
     // (S-1) stages of operand bytes in flight per workgroup: what the memory-bound short-K GEMMs
     // need (bandwidth = bytes in flight / latency).
     constexpr int S = C::STAGES, D = S - 1;
-    constexpr int LPS = stage_loads<C::BM, C::NW>() + stage_loads<C::BN, C::NW>();
+    constexpr int LPS = stage_loads<C::BM, C::NW, BK>() + stage_loads<C::BN, C::NW, BK>();
 #pragma unroll
     for (int i = 0; i < D; ++i)
       if (i < nk) {
@@ -240,7 +265,10 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
       if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
       else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
       else if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      // raw barrier: __syncthreads() would make the compiler drain every in-flight DMA (vmcnt(0)) here,
+      // collapsing the ring to one stage of prefetch (cdna_hip_programming.md, glds pipelining rules)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
       if (kt + D < nk) {
         const int sd = slot == 0 ? S - 1 : slot - 1;  // (kt + D) % S
         sta(smem + sd * C::STAGE_BYTES, kbeg + (kt + D) * BK);
@@ -273,8 +301,9 @@ __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* s
                                          int kend, f32x4 (&acc)[4][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  mainloop_st<C, AKC, BKC>([&](lds_char* t, int k0) { stage<AKC, C::BM, SA, C::NW>(sa, t, bm0, k0, wave, lane); },
-                           [&](lds_char* t, int k0) { stage<BKC, C::BN, SB, C::NW>(sb, t, bn0, k0, wave, lane); },
+  mainloop_st<C, AKC, BKC>(
+      [&](lds_char* t, int k0) { stage<AKC, C::BM, SA, C::NW, C::BK>(sa, t, bm0, k0, wave, lane); },
+      [&](lds_char* t, int k0) { stage<BKC, C::BN, SB, C::NW, C::BK>(sb, t, bn0, k0, wave, lane); },
                            smem, kbeg, kend, acc);
 }
 

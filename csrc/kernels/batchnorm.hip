@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
                                                            float* __restrict__ rvar, float* __restrict__ smean,
                                                            float* __restrict__ sinv, float momentum, float eps,
                                                            float* __restrict__ coef, float* __restrict__ dgamma,
-                                                           float* __restrict__ dbeta) {
+                                                           float* __restrict__ dbeta, int zero_after = 0) {
   constexpr int G = 16;  // chunk groups per channel
   __shared__ double sh[2][G][64];
   const int cl = threadIdx.x % 64, r = threadIdx.x / 64;
@@ -132,6 +132,13 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
     if (k < nchunk) {
       s0 += part[((long long)k * 2 + 0) * C + c];
       q0 += part[((long long)k * 2 + 1) * C + c];
+    }
+    if (zero_after) {  // epilogue-statistics slots come from a reused pool: leave them zeroed
+      float* pz = const_cast<float*>(part);
+      for (int kk = r; kk < nchunk; kk += G) {
+        pz[((long long)kk * 2 + 0) * C + c] = 0.f;
+        pz[((long long)kk * 2 + 1) * C + c] = 0.f;
+      }
     }
   }
   sh[0][r][cl] = (double)s0 + (double)s1;
@@ -219,6 +226,52 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
     load8_bf16(x + o0, a0);
     if constexpr (RES) load8_bf16(res + o0, r0);
     finish(a0, r0, o0);
+  }
+}
+
+// ---- fwd, projection blocks: out = relu(bn3(x) + bn_d(r)), both BNs applied in one pass ---------
+template <int TPR>
+__global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                         bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                         const float* __restrict__ coef2, long long M, int C,
+                                                         long long rpc) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  if (c0 >= C) return;
+  float sc[8], sf[8], sc2[8], sf2[8];
+  load8_f32(coef + c0, sc);
+  load8_f32(coef + C + c0, sf);
+  load8_f32(coef2 + c0, sc2);
+  load8_f32(coef2 + C + c0, sf2);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sf[k] += sf2[k];
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  long long m = m0 + ty;
+  for (; m + RPP < m1; m += 2 * RPP) {
+    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
+    float a0[8], a1[8], b0[8], b1[8];
+    load8_bf16(x + o0, a0);
+    load8_bf16(x + o1, a1);
+    load8_bf16(r + o0, b0);
+    load8_bf16(r + o1, b1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a0[k] = fmaxf(fmaf(a0[k], sc[k], fmaf(b0[k], sc2[k], sf[k])), 0.f);
+      a1[k] = fmaxf(fmaf(a1[k], sc[k], fmaf(b1[k], sc2[k], sf[k])), 0.f);
+    }
+    store8_bf16(y + o0, a0);
+    store8_bf16(y + o1, a1);
+  }
+  if (m < m1) {
+    const long long o0 = m * C + c0;
+    float a0[8], b0[8];
+    load8_bf16(x + o0, a0);
+    load8_bf16(r + o0, b0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a0[k] = fmaxf(fmaf(a0[k], sc[k], fmaf(b0[k], sc2[k], sf[k])), 0.f);
+    store8_bf16(y + o0, a0);
   }
 }
 
@@ -383,7 +436,7 @@ void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float
                       int C, float momentum, float eps, int relu, hipStream_t st) {
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                    sinv, momentum, eps, ws, nullptr, nullptr);
+                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1);
   bn_apply_launch(g, x, res, y, ws, M, C, relu, st);
 }
 
@@ -445,6 +498,21 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
   });
 }
 
+// Two BNs from epilogue partials applied in one pass: y = relu(bn(x) + bn2(r)) (projection blocks).
+void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* part, const float* part2,
+                       const float* gamma, const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
+                       const float* gamma2, const float* beta2, float* rmean2, float* rvar2, float* smean2,
+                       float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, 0, gamma2, beta2, rmean2, rvar2,
+                                                    smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
+  DTG_TPR_SWITCH(g.tpr, bn_apply2_kernel<T><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa));
+}
+
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
@@ -452,7 +520,7 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
-                                                    0.f, ws, dgamma, dbeta);
+                                                    0.f, ws, dgamma, dbeta, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {

@@ -268,6 +268,7 @@ struct DgradSB {
 template <class CF, int BNMODE = 0>
 __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
+  static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -295,6 +296,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
 template <class CF, int BNMODE = 0>
 __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
+  static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -322,6 +324,7 @@ template <class CF>
 __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ x, float* __restrict__ ws,
                                                            int tiles_n, int k_per_split) {
+  static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -350,6 +353,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideC
                                                              const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ w, Epi e, int tiles_n,
                                                              BnEpi bn) {
+  static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
   const StrideClass S = SC.c[blockIdx.y];

@@ -8,64 +8,13 @@
 // (= batch*H*W) is huge and whose output is a handful of tiles.
 #include "dtg/common.h"
 #include "dtg/kernels.h"
-#include "dtg/mfma_gemm.cuh"
-#include "dtg/gemm_epi.cuh"
-#include "dtg/bn_epi.cuh"
+#include "dtg/gemm_launch.cuh"
 #include <stdlib.h>
 #include <type_traits>
 
 namespace dtg {
 using namespace gemm;
 
-template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false>
-__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
-                                                     int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
-                                                     BnEpi bn) {
-  __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
-  lds_char* smem = (lds_char*)smem_raw;
-  if (bt.count > 1) {  // batched problem z: offset the operands (element strides)
-    const int zb = blockIdx.z / bt.nh, zh = blockIdx.z % bt.nh;
-    sa.p += zb * bt.sa_b + zh * bt.sa_h;
-    sb.p += zb * bt.sb_b + zh * bt.sb_h;
-    const long long co = zb * bt.sc_b + zh * bt.sc_h;
-    e.C = (char*)e.C + co * (e.c_bf16 ? 2 : 4);
-    if (e.aux) e.aux = (char*)e.aux + co * 2;
-  }
-  const int ntiles = gridDim.x;  // tiles per split
-  const int t = xcd_remap(blockIdx.x, ntiles);
-  const int tm = t / tiles_n, tn = t % tiles_n;
-  const int bm0 = tm * CF::BM, bn0 = tn * CF::BN;
-  const int split = blockIdx.y;
-  const int kbeg = split * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
-  if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
-    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, N, e, bn, t, [](int m) { return m; });
-    return;
-  }
-  if (split_k > 1) {
-    float* slab = ws + (long long)split * M * N;
-    const bool vec = (N & 3) == 0;
-    epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
-      float* p = slab + (long long)m * N + n;
-      if (vec && n + 8 <= N) store8_f32(p, v);
-      else
-        for (int k = 0; k < 8 && n + k < N; ++k) p[k] = v[k];
-    });
-    return;
-  }
-  if constexpr (FAST) {  // bf16, aligned, no bias/act/aux (fast_epi() checked): no per-group switches
-    auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); };
-    epilogue_staged<CF, decltype(op), !SA::kGuard && !SB::kGuard>(smem, acc, bm0, bn0, M, N, op);
-  } else {
-    epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
-  }
-}
 
 // Split-K reduction: a thread owns 8 consecutive outputs and sums their split_k partials; the
 // split loop is unrolled by 4 so 4 x 32 B of loads are in flight per thread (the reduce is a pure
@@ -155,44 +104,6 @@ int gemm_pick_split(int M, int N, int K) {
   return s;
 }
 
-// epilogue specialisation: bf16 output, 16-B aligned 8-column groups, no bias / activation / aux
-static bool fast_epi(const Epi& e, int N) {
-  return e.c_bf16 && !e.bias && e.act == 0 && e.aux_mode == 0 && (e.ldc % 8) == 0 && (N % 8) == 0 &&
-         ((uintptr_t)e.C % 16) == 0;
-}
-
-template <class CF, bool AK, bool BK_, bool GUARD>
-static void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
-                   int kps, const Epi& e, float* ws, hipStream_t st, const GemmBatch& bt) {
-  using SA = std::conditional_t<AK, DenseKC<GUARD>, DenseMC<GUARD>>;
-  using SB = std::conditional_t<BK_, DenseKC<GUARD>, DenseMC<GUARD>>;
-  SA sa{A, lda, M, K};
-  SB sb{B, ldb, N, K};
-  const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  dim3 grid(tiles_m * tiles_n, split_k, bt.count);
-  if constexpr (AK) {  // (K-contiguous A = forward / dgrad GEMMs; weight gradients go through split-K)
-    if (split_k == 1 && fast_epi(e, N) && (bt.count == 1 || ((bt.sc_b | bt.sc_h) & 7) == 0)) {
-      hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB, 0, true>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K,
-                         tiles_n, split_k, kps, e, ws, bt, BnEpi());
-      if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                       kps, e, ws, bt, BnEpi());
-  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
-}
-
-template <class CF, bool GUARD>
-static void launch_layout(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
-                          int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
-                          const GemmBatch& bt) {
-  if (a_kc && b_kc) launch<CF, true, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else if (a_kc) launch<CF, true, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else if (b_kc) launch<CF, false, true, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else launch<CF, false, false, GUARD>(A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-}
-
 template <int BM_, int BN_>
 static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
                        int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
@@ -251,16 +162,11 @@ static void launch_big(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
 }
 
-template <class CF>
-static void launch_exact(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
-                         int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
-                         const GemmBatch& bt) {
-  const bool full = (M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0);
-  if (full) launch_layout<CF, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-}
 
-// DTG_GEMM_CFG=<n> forces one tile configuration (tools/gemm_sweep.py A/B sweeps); 0 = heuristic
+// forced tile configurations (tools/gemm_sweep.py): gemm_forced.hip
+bool gemm_launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb,
+                        int M, int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
+                        const GemmBatch& bt);
 static int g_forced_cfg = -1;
 static int forced_cfg() {
   if (g_forced_cfg < 0) {
@@ -270,34 +176,6 @@ static int forced_cfg() {
   return g_forced_cfg;
 }
 void gemm_force_cfg(int cfg) { g_forced_cfg = cfg; }
-
-static bool launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B,
-                          long long ldb, int M, int N, int K, int split_k, int kps, const Epi& e, float* ws,
-                          hipStream_t st, const GemmBatch& bt) {
-#define DTG_CFG_CASE(n, ...)                                                                          \
-  case n:                                                                                            \
-    launch_exact<__VA_ARGS__>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt); \
-    return true;
-  switch (cfg) {
-    DTG_CFG_CASE(1, Cfg<128, 128, 1>)
-    DTG_CFG_CASE(2, Cfg<128, 128, 2>)
-    DTG_CFG_CASE(3, Cfg<128, 128, 3>)
-    DTG_CFG_CASE(4, Cfg<128, 128, 4>)
-    DTG_CFG_CASE(5, Cfg<256, 64, 2>)
-    DTG_CFG_CASE(6, Cfg<256, 64, 3>)
-    DTG_CFG_CASE(7, Cfg<256, 64, 4>)
-    DTG_CFG_CASE(8, Cfg<256, 128, 3, 8>)
-    DTG_CFG_CASE(9, Cfg<256, 128, 2, 8>)
-    DTG_CFG_CASE(10, Cfg<128, 256, 2, 8>)
-    DTG_CFG_CASE(11, Cfg<128, 256, 3, 8>)
-    DTG_CFG_CASE(12, Cfg<64, 256, 2>)
-    DTG_CFG_CASE(13, Cfg<64, 256, 3>)
-    DTG_CFG_CASE(14, Cfg<256, 64, 1>)
-    DTG_CFG_CASE(15, Cfg<64, 256, 1>)
-    default: return false;
-  }
-#undef DTG_CFG_CASE
-}
 
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
   if (N % 8 == 0 && split_k > 16) {
@@ -326,7 +204,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
       gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
       return;
     }
-    if (launch_forced(fc, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt)) return;
+    if (gemm_launch_forced(fc, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt)) return;
   }
   if (bt.count == 1 && use_8phase(M, N, K, split_k)) {
     gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
@@ -341,7 +219,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     return;
   }
   // Tile width follows N so the streamed activation operand A is read as few times as possible:
-  // 256x64 for N <= 64, 128x128 for N = 128, 64x256 for N >= 256.  LDS ring depth: a single stage
+  // 256x64 for N <= 64, 64x256 for N >= 256 with K <= 256, else 128x128 (r01_tiles sweeps).  LDS ring depth: a single stage
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
   // (< 512 tiles) and K long enough (>= 2048) that in-block prefetch pays (profiles/r01_tiles).
   const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * split_k * bt.count;
@@ -352,7 +230,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     launch_exact<Cfg<128, 128, 2>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else if (skinny(N)) {
     launch_exact<Cfg<256, 64, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  } else if (N >= 256 && M >= 64) {
+  } else if (N >= 256 && M >= 64 && kps <= 256) {
     launch_exact<Cfg<64, 256, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else {
     launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
@@ -387,7 +265,7 @@ static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, lo
   const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
   if (tiles128 < 512 && K >= 2048) launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (skinny(N)) launch_bn_cfg<Cfg<256, 64, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else if (N >= 256 && M >= 64) launch_bn_cfg<Cfg<64, 256, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (N >= 256 && M >= 64 && K <= 256) launch_bn_cfg<Cfg<64, 256, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 

@@ -87,14 +87,14 @@ class _BottleneckFn(torch.autograd.Function):
         b1, b2, b3 = blk.c1.bn, blk.c2.bn, blk.c3.bn
         w1, w2, w3 = blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight
         if _FUSE:
-            y1, p1 = L.gemm_bn(x2, _mat(w1), 1)
+            y1, p1 = L.gemm_bn(x2, _mat(w1), 1, pooled=True)
             a1, m1, i1 = L.bn_fwd_part(y1, p1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var,
                                        b1.momentum, b1.eps, True)
-            y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1)
+            y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1, pooled=True)
             y2 = y2.view(-1, width)
             a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
                                        b2.momentum, b2.eps, True)
-            y3, p3 = L.gemm_bn(a2, _mat(w3), 1)
+            y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
         else:
             y1 = gemm(x2, True, _mat(w1), True)
             a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
@@ -108,12 +108,11 @@ class _BottleneckFn(torch.autograd.Function):
             bd, wd = blk.down.bn, blk.down.conv.weight
             if _FUSE:
                 if st == 1:
-                    yd, pd = L.gemm_bn(x2, _mat(wd), 1)
+                    yd, pd = L.gemm_bn(x2, _mat(wd), 1, pooled=True)
                 else:
-                    yd, pd = L.conv_fwd_bn(x2.view(n, h, w, c), _krsc(wd), st, 0)
+                    yd, pd = L.conv_fwd_bn(x2.view(n, h, w, c), _krsc(wd), st, 0, pooled=True)
                     yd = yd.view(-1, cout)
-                idn, md, idd = L.bn_fwd_part(yd, pd, None, bd.weight, bd.bias, bd.running_mean, bd.running_var,
-                                             bd.momentum, bd.eps, False)
+                idn = None  # applied together with BN3 below (no materialised identity branch)
             else:
                 if st == 1:
                     yd = gemm(x2, True, _mat(wd), True)
@@ -123,7 +122,12 @@ class _BottleneckFn(torch.autograd.Function):
                                               bd.momentum, bd.eps, False)
         else:
             idn = x2
-        if _FUSE:
+        if _FUSE and blk.down is not None:  # out = relu(bn3(y3) + bn_d(yd)) in one pass
+            assert bd.momentum == b3.momentum and bd.eps == b3.eps
+            out, m3, i3, md, idd = L.bn_fwd2_part(y3, p3, b3.weight, b3.bias, b3.running_mean, b3.running_var, yd, pd,
+                                                  bd.weight, bd.bias, bd.running_mean, bd.running_var, b3.momentum,
+                                                  b3.eps)
+        elif _FUSE:
             out, m3, i3 = L.bn_fwd_part(y3, p3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var,
                                         b3.momentum, b3.eps, True)
         else:
@@ -161,13 +165,15 @@ class _BottleneckFn(torch.autograd.Function):
             dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
             dres = do  # our own buffer (pointer-checked above): dx accumulates into it in place
         else:
+            if lk is not None and lk.part is not None:
+                lk.part.zero_()  # pooled slots must go back zeroed (see bn_part in csrc/bindings/ops.cc)
             dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)],
                                        g[id(b3.bias)])
         if lk is not None:
             lk.part = lk.dp = None
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
         if _FUSE:
-            dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias)
+            dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
         gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
@@ -178,7 +184,8 @@ class _BottleneckFn(torch.autograd.Function):
             dy2 = L.bn_bwd(da2, a2, y2, b2.weight, m2, i2, True, False, g[id(b2.weight)], g[id(b2.bias)])[0]
         dy2_4 = dy2.view(n, p_, q_, width)
         if _FUSE:
-            dp1, q1 = L.conv_dgrad_bn(dy2_4, _krsc(w2).contiguous(), h, w, st, 1, y1, m1, i1, b1.weight, b1.bias)
+            dp1, q1 = L.conv_dgrad_bn(dy2_4, _krsc(w2).contiguous(), h, w, st, 1, y1, m1, i1, b1.weight, b1.bias,
+                                       pooled=True)
             dp1 = dp1.view(-1, width)
         else:
             da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
@@ -217,7 +224,7 @@ class _BottleneckFn(torch.autograd.Function):
         if not dx_done:
             if lk_in is not None:  # mode 3: finish the previous block's BN3 reduction in this epilogue
                 _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                    mask=x2, out=dx2)
+                                    mask=x2, out=dx2, pooled=True)
                 lk_in.part, lk_in.dp = part, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)

@@ -133,3 +133,30 @@ def test_bn_part_matches_unfused(res):
     dx1, _, dg1, db1 = L.bn_bwd_part(dp, y, pr.view(-1), gamma, m0, i0, False, None, None)
     assert _rel(dg1, dg0) < 1e-3 and _rel(db1, db0) < 1e-3
     assert _rel(dx1, dx0) < 1e-2
+
+
+def test_bn_fwd2_part_matches_two_passes():
+    """relu(bn3(y3) + bn_d(yd)) in one pass == bn_d applied, then bn3 with the residual."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(4)
+    M, K, N = 2048, 128, 256
+    L = lib()
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w3 = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    wd = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    ch = lambda: ((torch.rand(N, generator=g) + 0.5).to(dev), (torch.randn(N, generator=g) * 0.1).to(dev))  # noqa
+    (g3, b3), (gd, bd) = ch(), ch()
+    outs = []
+    for fused in (False, True):
+        y3, p3 = L.gemm_bn(a, w3, 1)
+        yd, pd = L.gemm_bn(a, wd, 1)
+        rm3, rv3, rmd, rvd = (torch.zeros(N, device=dev), torch.ones(N, device=dev), torch.zeros(N, device=dev),
+                              torch.ones(N, device=dev))
+        if fused:
+            o, m3, i3, md, idd = L.bn_fwd2_part(y3, p3, g3, b3, rm3, rv3, yd, pd, gd, bd, rmd, rvd, 0.1, 1e-5)
+        else:
+            idn, md, idd = L.bn_fwd_part(yd, pd, None, gd, bd, rmd, rvd, 0.1, 1e-5, False)
+            o, m3, i3 = L.bn_fwd_part(y3, p3, idn, g3, b3, rm3, rv3, 0.1, 1e-5, True)
+        outs.append((o, m3, i3, md, idd, rm3, rv3, rmd, rvd))
+    for x, y in zip(outs[1], outs[0]):
+        assert _rel(x, y) < 1e-2

@@ -21,7 +21,9 @@ from dtg.ops._native import lib  # noqa: E402
 
 NAMES = {0: "heur", 1: "128x128s1", 2: "128x128s2", 3: "128x128s3", 4: "128x128s4", 5: "256x64s2", 6: "256x64s3",
          7: "256x64s4", 8: "256x128s3w8", 9: "256x128s2w8", 10: "128x256s2w8", 11: "128x256s3w8", 12: "64x256s2",
-         13: "64x256s3", 14: "256x64s1", 15: "64x256s1", 99: "8phase"}
+         13: "64x256s3", 14: "256x64s1", 15: "64x256s1", 16: "128x128s2k32",
+         17: "128x128s3k32", 18: "128x128s4k32", 19: "64x256s3k32", 20: "256x64s3k32", 21: "64x256s2k32",
+         22: "256x64s2k32", 23: "128x128s5k32", 24: "64x256s4k32", 99: "8phase"}
 
 # (M, N, K, a_kc, b_kc, beta): the memory-bound and mid-size GEMMs of a ResNet-50 batch-256 step
 SHAPES = [
@@ -54,7 +56,7 @@ def timeit(fn, iters=10, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default="")
-    ap.add_argument("--cfgs", default="0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,99")
+    ap.add_argument("--cfgs", default="0,1,2,3,14,15,16,17,18,19,20,21,22,23,24")
     ap.add_argument("--shapes", default="", help="comma list of shape indices (default all)")
     a = ap.parse_args()
     L = lib()
@@ -71,7 +73,7 @@ def main():
         fl = 2.0 * M * N * K
         rows = []
         for c in cfgs:
-            if c in (5, 6, 7, 14) and N > 64 and N % 64:
+            if c in (5, 6, 7, 14, 20, 22) and N > 64 and N % 64:
                 continue
             L.gemm_force_cfg(c)
             out = torch.zeros_like(C)

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Steady-state per-step kernel breakdown from a rocprofv3 --kernel-trace run of bench.py.
+
+Warmup dispatches (MIOpen find, first-touch allocations) are dropped by keeping only the kernels
+after the (skip+1)-th softmax-xent launch (one per training step), so the table is per timed step.
+
+    python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv [--skip 4] [--top 40] [--out f.md]
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def short(name):
+    m = re.search(r"dtg::(\w+?)_kernel", name) or re.search(r"dtg::(\w+)", name)
+    if m:
+        base = m.group(1)
+        c = re.search(r"Cfg<(\d+), (\d+), (\d+), (\d+)(?:, (\d+))?>", name)
+        mode = re.search(r"Cfg<[^>]*>, (?:true|false), (?:true|false), [^,]+, [^,]+, (\d)", name)
+        if c:
+            base += f" {c.group(1)}x{c.group(2)}s{c.group(3)}"
+        if mode and mode.group(1) != "0":
+            base += f" bn{mode.group(1)}"
+        return base
+    return name[:48]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--skip", type=int, default=4, help="warmup steps to drop")
+    ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "softmax_xent" in r["Kernel_Name"]]
+    if len(marks) <= a.skip + 1:
+        raise SystemExit(f"only {len(marks)} steps in the trace")
+    lo, hi = marks[a.skip], marks[-1]
+    steps = len(marks) - 1 - a.skip
+    seg = rows[lo + 1:hi + 1]
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for r in seg:
+        k = short(r["Kernel_Name"])
+        agg[k][0] += 1
+        agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    busy = sum(v[1] for v in agg.values()) / steps
+    wall = (int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])) / 1e3 / steps
+    lines = [f"steady-state step: wall {wall / 1e3:.2f} ms, kernel-busy {busy / 1e3:.2f} ms over {steps} steps",
+             f"{'kernel':44s} {'calls/step':>10s} {'ms/step':>8s} {'%':>5s}"]
+    for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        lines.append(f"{k:44s} {n / steps:10.1f} {us / steps / 1e3:8.3f} {100 * us / steps / busy:5.1f}")
+    txt = "\n".join(lines)
+    print(txt)
+    if a.out:
+        open(a.out, "w").write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
