@@ -11,6 +11,10 @@ workers intra-node (RCCL send/recv)").  Reference semantics kept:
 * DOWNPOUR / ADAG window (``DOWNPOUR/DOWNPOUR.py:63-102``, ``ADAG/ADAG.py:69-90``): a worker runs
   ``window`` local steps (optionally applying a local optimizer), accumulates their gradients and
   pushes the sum (DOWNPOUR) or the mean (ADAG); the PS applies it with the global optimizer.
+* Dynamic SGD (the reference README's TODO list, ``README.md:40``): ``staleness_scaling="dyn"``
+  scales every update by 1/(tau+1), tau = the number of PS updates since the pushing worker last
+  pulled (DynSGD, Jiang et al., SIGMOD 2017), so stale gradients from slow workers move the
+  parameters less.
 
 MI355X design: parameters and optimizer state live in the PS GPU's flat buffers (FlatParams); a
 push is one RCCL send per dtype group (bf16 compute grads + fp32 norm/bias grads), a pull is one
@@ -106,7 +110,10 @@ class AsyncPSWorker:
 class AsyncPSServer:
     """PS side: ``serve()`` runs until every worker sent DONE; returns the number of updates."""
 
-    def __init__(self, flat, optimizer, workers, window=1, window_mode="sum", group=None, staleness_log=False):
+    def __init__(self, flat, optimizer, workers, window=1, window_mode="sum", group=None, staleness_log=False,
+                 staleness_scaling=None):
+        assert staleness_scaling in (None, "dyn")
+        self.dyn = staleness_scaling == "dyn"
         self.flat = flat
         self.opt = optimizer
         self.workers = list(workers)
@@ -122,6 +129,7 @@ class AsyncPSServer:
         self.version = 0
         self._pulled_version = {w: 0 for w in self.workers}
         self.staleness = [] if staleness_log else None
+        self.scales = [] if staleness_log else None
         self.per_worker = {w: 0 for w in self.workers}
 
     def _send_params(self, w):
@@ -136,15 +144,18 @@ class AsyncPSServer:
     def _apply(self, w):
         bufs = self._recv[w]
         saved = [g.grad for g in self.flat]
+        tau = self.version - self._pulled_version[w]
+        scale = self.gscale / (tau + 1) if self.dyn else self.gscale
         try:
             for g, b in zip(self.flat, bufs):
                 g.grad = b
-            self.opt.step(grad_scale=self.gscale, zero_grad=False)
+            self.opt.step(grad_scale=scale, zero_grad=False)
         finally:
             for g, s in zip(self.flat, saved):
                 g.grad = s
         if self.staleness is not None:
-            self.staleness.append(self.version - self._pulled_version[w])
+            self.staleness.append(tau)
+            self.scales.append(scale)
         self.version += 1
         self.updates += 1
         self.per_worker[w] += 1

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--window", type=int, default=1)
     ap.add_argument("--window_mode", default="sum", choices=("sum", "mean"))
+    ap.add_argument("--dyn_sgd", action="store_true",
+                    help="Dynamic SGD: scale each PS update by 1/(staleness+1) (reference README TODO)")
     ap.add_argument("--tiny", action="store_true", help="narrow 4-block ResNet, 32x32 images (CPU smoke tests)")
     a, _ = ap.parse_known_args()
     cluster = {"ps": [f"localhost:{a.base_port}"],
@@ -47,7 +49,7 @@ def main():
     if a.job_name == "ps":
         opt = FusedSGD(flat, lr=a.lr, momentum=0.9, weight_decay=5e-5)
         ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, window_mode=a.window_mode,
-                           staleness_log=True)
+                           staleness_log=True, staleness_scaling="dyn" if a.dyn_sgd else None)
         t0 = time.time()
         n = ps.serve()
         dt = time.time() - t0

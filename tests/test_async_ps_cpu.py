@@ -34,7 +34,7 @@ def _data(seed):
     return torch.randn(32, 8, generator=g), torch.randint(0, 3, (32,), generator=g)
 
 
-def _rank(rank, world, port, steps, window, mode, q):
+def _rank(rank, world, port, steps, window, mode, q, dyn=False):
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -50,11 +50,11 @@ def _rank(rank, world, port, steps, window, mode, q):
         if rank == 0:
             opt = FusedSGD(flat, lr=0.1, momentum=0.0)
             ps = AsyncPSServer(flat, opt, workers=range(1, world), window=window, window_mode=mode,
-                               staleness_log=True)
+                               staleness_log=True, staleness_scaling="dyn" if dyn else None)
             n = ps.serve()
             q.put((rank, "ok", {"updates": n, "per_worker": dict(ps.per_worker),
                                 "w": [t.clone() for t in (g.master for g in flat)],
-                                "staleness": list(ps.staleness)}))
+                                "staleness": list(ps.staleness), "scales": list(ps.scales)}))
         else:
             w = AsyncPSWorker(flat, ps_rank=0, window=window, window_mode=mode)
             w.begin()
@@ -74,13 +74,13 @@ def _rank(rank, world, port, steps, window, mode, q):
         raise
 
 
-def _run(world, steps, window=1, mode="sum"):
+def _run(world, steps, window=1, mode="sum", dyn=False):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _cluster import free_ports
     port = free_ports(1)[0]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, steps, window, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, steps, window, mode, q, dyn)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -239,4 +239,23 @@ def test_easgd_two_workers_learn():
     out = _run_elastic(3, 24, 4, 0.3)
     assert out[0]["updates"] == 2 * (24 // 4)
     for r in (1, 2):
+        assert out[r]["losses"][-1] < out[r]["losses"][0]
+
+
+def test_dynsgd_scales_updates_by_staleness():
+    """Dynamic SGD (reference README TODO): every PS update is scaled by 1/(staleness+1); with one
+    worker the staleness is always 0, so it equals the sequential replay; with three workers stale
+    pushes occur and are damped accordingly."""
+    out = _run(2, steps=8, dyn=True)
+    assert set(out[0]["staleness"]) == {0} and all(s == 1.0 for s in out[0]["scales"])
+    ref = _replay(8, 1, "sum")
+    got = _ps_params_by_name(out)
+    for n, p in ref.items():
+        assert torch.allclose(got[n], p, atol=1e-5), n
+    out = _run(4, steps=10, dyn=True)
+    assert out[0]["updates"] == 30
+    assert max(out[0]["staleness"]) > 0
+    for tau, sc in zip(out[0]["staleness"], out[0]["scales"]):
+        assert abs(sc - 1.0 / (tau + 1)) < 1e-12
+    for r in (1, 2, 3):
         assert out[r]["losses"][-1] < out[r]["losses"][0]

@@ -33,6 +33,13 @@ def main():
         fn = (lambda: L.gemm_bn(A, W, 1)) if op == "gemm_bn1" else (lambda: L.gemm(A, True, W, True, out, 1.0, 0.0,
                                                                                      None, 0, 1))
         fl = 2.0 * M * N * K
+    elif op == "wgrad":  # dW[M,N] (+)= dY^T X: dY [K,M], X [K,N] both MN-contiguous, auto split-K, fp32 out
+        M, N, K = a
+        A = torch.randn(K, M, device=dev, dtype=bf)
+        B = torch.randn(K, N, device=dev, dtype=bf)
+        out = torch.zeros(M, N, device=dev, dtype=torch.float32)
+        fn = lambda: L.gemm(A, False, B, False, out, 1.0, 1.0, None, 0, 0)  # noqa: E731
+        fl = 2.0 * M * N * K
     elif op in ("gemm_bn2",):
         M, N, K = a
         A = torch.randn(M, K, device=dev, dtype=bf)

@@ -12,16 +12,18 @@ import sys
 
 
 def load(case_dir):
-    vals = collections.defaultdict(list)
+    """{kernel name: ({counter: mean over dispatches}, meta)} for the dtg kernels of one case."""
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
     for f in glob.glob(os.path.join(case_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "dtg::" not in r["Kernel_Name"]:
                 continue
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            meta = {"kernel": r["Kernel_Name"][:90], "vgpr": r["VGPR_Count"], "agpr": r["Accum_VGPR_Count"],
-                    "lds": r["LDS_Block_Size"], "grid": r["Grid_Size"], "wg": r["Workgroup_Size"]}
-    return {k: sum(v) / len(v) for k, v in vals.items()}, meta
+            k = r["Kernel_Name"][:110]
+            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta[k] = {"vgpr": r["VGPR_Count"], "agpr": r["Accum_VGPR_Count"], "lds": r["LDS_Block_Size"],
+                       "grid": r["Grid_Size"], "wg": r["Workgroup_Size"]}
+    return {k: ({c: sum(v) / len(v) for c, v in d.items()}, meta[k]) for k, d in vals.items()}
 
 
 def main():
@@ -29,10 +31,8 @@ def main():
     out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
     lines = []
     for case in sorted(os.listdir(root)):
-        c, m = load(os.path.join(root, case))
-        if not c:
-            continue
-        lines.append(f"## {case}\n{m}")
+      for kname, (c, m) in load(os.path.join(root, case)).items():
+        lines.append(f"## {case}: {kname}\n{m}")
         wc = c.get("SQ_WAVE_CYCLES", 0) or 1
         for k in sorted(c):
             lines.append(f"  {k:24s} {c[k]:16.0f}")
