@@ -166,3 +166,23 @@ def test_direct_write_params_count_once():
         p.join(120)
     res = dict(q.get(timeout=5) for _ in range(2))
     assert res == {0: "ok", 1: "ok"}, res
+
+
+def test_allreduce_bw_tool_gloo(tmp_path):
+    """tools/allreduce_bw.py runs end to end on 2 gloo ranks and reports sane bandwidth rows."""
+    import json as _json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "bw.jsonl"
+    sys.path.insert(0, os.path.join(root, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(root, "tools", "allreduce_bw.py"), "--min_kb", "4",
+           "--max_mb", "0.25", "--iters", "3", "--warmup", "1", "--bucket_mb", "40", "--json", str(out)]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES=""))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    rows = [_json.loads(line) for line in out.read_text().splitlines()]
+    assert len(rows) >= 7 and all(x["n_ranks"] == 2 and x["us"] > 0 and x["busbw_GBs"] > 0 for x in rows)
+    assert rows[-1]["tag"].startswith("resnet50_bucket")
