@@ -435,10 +435,15 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
     if (mode == 3) {
       TORCH_CHECK(mask.has_value() && mask->defined(), "mode 3 needs the mask tensor");
       CHECK_IN(*mask);
-      CHECK_DT(*mask, at::kBFloat16);
-      TORCH_CHECK(mask->numel() == (long long)M * N, "mask shape mismatch");
       bn.mode = 3;
-      bn.mask = cbfp(*mask);
+      if (mask->scalar_type() == at::kByte) {  // packed bits [M, N/8]
+        TORCH_CHECK(mask->numel() == (long long)M * (N / 8), "mask bits shape mismatch");
+        bn.maskbits = mask->data_ptr<uint8_t>();
+      } else {
+        CHECK_DT(*mask, at::kBFloat16);
+        TORCH_CHECK(mask->numel() == (long long)M * N, "mask shape mismatch");
+        bn.mask = cbfp(*mask);
+      }
     }
   } else {
     bn.part = part.data_ptr<float>();
@@ -488,9 +493,17 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t
   return {dx, part};
 }
 
+uint8_t* bits_ptr(const c10::optional<Tensor>& bits, long long M, int C) {
+  if (!bits.has_value() || !bits->defined()) return nullptr;
+  CHECK_IN(*bits);
+  TORCH_CHECK(bits->scalar_type() == at::kByte && bits->numel() == M * (C / 8), "bits must be uint8 [M, C/8]");
+  return bits->data_ptr<uint8_t>();
+}
+
+// bits (optional uint8 [M, C/8]) receives the packed (out > 0) relu mask
 std::tuple<Tensor, Tensor, Tensor> bn_fwd_part(Tensor x, Tensor part, c10::optional<Tensor> res, Tensor gamma,
                                                Tensor beta, Tensor rmean, Tensor rvar, double momentum, double eps,
-                                               bool relu) {
+                                               bool relu, c10::optional<Tensor> bits) {
   CHECK_IN(x);
   CHECK_DT(x, at::kBFloat16);
   TORCH_CHECK(x.dim() == 2, "x must be [M, C]");
@@ -518,7 +531,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_part(Tensor x, Tensor part, c10::optio
   dtg::bn_fwd_from_part(cbfp(x), has_res ? cbfp(*res) : nullptr, bfp(y), gamma.data_ptr<float>(),
                         beta.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
                         smean.data_ptr<float>(), sinv.data_ptr<float>(), part.data_ptr<float>(), ws.data_ptr<float>(),
-                        M, C, (float)momentum, (float)eps, relu, cur_stream());
+                        M, C, (float)momentum, (float)eps, relu, cur_stream(), bits_ptr(bits, M, C));
   return {y, smean, sinv};
 }
 
@@ -526,7 +539,8 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_part(Tensor x, Tensor part, c10::optio
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> bn_fwd2_part(Tensor x, Tensor part, Tensor gamma, Tensor beta,
                                                                 Tensor rmean, Tensor rvar, Tensor r, Tensor part2,
                                                                 Tensor gamma2, Tensor beta2, Tensor rmean2,
-                                                                Tensor rvar2, double momentum, double eps) {
+                                                                Tensor rvar2, double momentum, double eps,
+                                                                c10::optional<Tensor> bits) {
   CHECK_IN(x);
   CHECK_IN(r);
   CHECK_DT(x, at::kBFloat16);
@@ -555,7 +569,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> bn_fwd2_part(Tensor x, Tensor
                          rvar.data_ptr<float>(), m1.data_ptr<float>(), i1.data_ptr<float>(), gamma2.data_ptr<float>(),
                          beta2.data_ptr<float>(), rmean2.data_ptr<float>(), rvar2.data_ptr<float>(),
                          m2.data_ptr<float>(), i2.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)momentum,
-                         (float)eps, cur_stream());
+                         (float)eps, cur_stream(), bits_ptr(bits, M, C));
   return {y, m1, i1, m2, i2};
 }
 
@@ -647,8 +661,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),
         pybind11::arg("W"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("x"), pybind11::arg("mean"),
         pybind11::arg("invstd"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("pooled") = false);
-  m.def("bn_fwd2_part", &bn_fwd2_part);
-  m.def("bn_fwd_part", &bn_fwd_part);
+  m.def("bn_fwd2_part", &bn_fwd2_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("gamma"),
+        pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("r"), pybind11::arg("part2"),
+        pybind11::arg("gamma2"), pybind11::arg("beta2"), pybind11::arg("rmean2"), pybind11::arg("rvar2"),
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("bits") = pybind11::none());
+  m.def("bn_fwd_part", &bn_fwd_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("res"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
+        pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("bits") = pybind11::none());
   m.def("bn_bwd_part", &bn_bwd_part);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);

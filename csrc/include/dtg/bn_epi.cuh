@@ -71,7 +71,13 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       const long long off = (long long)row * e.ldc + n;
       float xv[8], mk[8], old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       load8_bf16(bn.x + off, xv);
-      load8_bf16(bn.mask + off, mk);
+      if (bn.maskbits) {
+        const uint32_t byte = bn.maskbits[(long long)row * (N >> 3) + (n >> 3)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mk[k] = (float)((byte >> k) & 1u);
+      } else {
+        load8_bf16(bn.mask + off, mk);
+      }
       if (e.beta != 0.f) load8_bf16((const bf16_t*)e.C + off, old);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {

@@ -42,20 +42,23 @@ struct BnEpi {
   const float* invstd = nullptr;
   const float* gamma = nullptr;
   const float* beta = nullptr;
-  const bf16_t* mask = nullptr;  // mode 3
+  const bf16_t* mask = nullptr;      // mode 3: relu mask as the bf16 block output (> 0) ...
+  const uint8_t* maskbits = nullptr; // ... or as packed bits [M][N/8] (bit k of byte n/8 = column n+k)
 };
 
 // ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
 long long bn_workspace_floats(long long M, int C);
 // finish a forward BN from fused-epilogue statistics: finalize (coef = ws[0:2C]) + apply
+// bits (optional, [M][C/8]): packed (y > 0) of the output, the relu mask a later backward re-reads
 void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                       float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
-                      int C, float momentum, float eps, int relu, hipStream_t st);
+                      int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits = nullptr);
 // y = relu(bn(x) + bn2(r)) with both BNs' statistics from epilogue partials (ws: 4C floats)
 void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* part, const float* part2,
                        const float* gamma, const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
                        const float* gamma2, const float* beta2, float* rmean2, float* rvar2, float* smean2,
-                       float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st);
+                       float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st,
+                       uint8_t* bits = nullptr);
 // finish a backward BN from mode-2 partials: dx = a*dp + bx*x + c0 (ws: 3C floats), dres = dp if given
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,

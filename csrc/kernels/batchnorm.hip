@@ -183,10 +183,18 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restri
 }
 
 // ---- pass 2 (fwd): apply scale/shift (+residual) (+relu) -------------------------------------
+__device__ __forceinline__ uint8_t pos_bits8(const float (&v)[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b |= (v[k] > 0.f ? 1u : 0u) << k;
+  return (uint8_t)b;
+}
+
 template <int TPR, bool RES, bool RELU>
 __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                         bf16_t* __restrict__ y, const float* __restrict__ coef,
-                                                        long long M, int C, long long rpc) {
+                                                        long long M, int C, long long rpc,
+                                                        uint8_t* __restrict__ bits = nullptr) {
   constexpr int RPP = kBlk / TPR, CW = TPR * 8;
   const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
   const int c0 = blockIdx.y * CW + tx * 8;
@@ -205,6 +213,7 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
       a[k] = v;
     }
     store8_bf16(y + off, a);
+    if (bits) bits[off >> 3] = pos_bits8(a);  // off = m*C + c0, both multiples of 8
   };
   long long m = m0 + ty;
   // 2 rows per iteration: all four 16-B loads are in flight before any math (memory-level parallelism)
@@ -234,7 +243,7 @@ template <int TPR>
 __global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                          bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                          const float* __restrict__ coef2, long long M, int C,
-                                                         long long rpc) {
+                                                         long long rpc, uint8_t* __restrict__ bits) {
   constexpr int RPP = kBlk / TPR, CW = TPR * 8;
   const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
   const int c0 = blockIdx.y * CW + tx * 8;
@@ -263,6 +272,10 @@ __global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restric
     }
     store8_bf16(y + o0, a0);
     store8_bf16(y + o1, a1);
+    if (bits) {
+      bits[o0 >> 3] = pos_bits8(a0);
+      bits[o1 >> 3] = pos_bits8(a1);
+    }
   }
   if (m < m1) {
     const long long o0 = m * C + c0;
@@ -272,6 +285,7 @@ __global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restric
 #pragma unroll
     for (int k = 0; k < 8; ++k) a0[k] = fmaxf(fmaf(a0[k], sc[k], fmaf(b0[k], sc2[k], sf[k])), 0.f);
     store8_bf16(y + o0, a0);
+    if (bits) bits[o0 >> 3] = pos_bits8(a0);
   }
 }
 
@@ -403,16 +417,16 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
   }
 
 static void bn_apply_launch(const BnGeom& g, const bf16_t* x, const bf16_t* res, bf16_t* y, const float* coef,
-                            long long M, int C, int relu, hipStream_t st) {
+                            long long M, int C, int relu, hipStream_t st, uint8_t* bits = nullptr) {
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
-      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
     } else {
-      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
-      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
     }
   });
 }
@@ -433,11 +447,11 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
 // Statistics already reduced by a GEMM / conv epilogue (kBnStatSlots partials): finalize + apply.
 void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                       float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
-                      int C, float momentum, float eps, int relu, hipStream_t st) {
+                      int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
                                                     sinv, momentum, eps, ws, nullptr, nullptr, 1);
-  bn_apply_launch(g, x, res, y, ws, M, C, relu, st);
+  bn_apply_launch(g, x, res, y, ws, M, C, relu, st, bits);
 }
 
 // Inference: coefficients from running statistics (tiny launch) then the same apply pass.
@@ -502,7 +516,8 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
 void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* part, const float* part2,
                        const float* gamma, const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
                        const float* gamma2, const float* beta2, float* rmean2, float* rvar2, float* smean2,
-                       float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st) {
+                       float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st,
+                       uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
                                                     sinv, momentum, eps, ws, nullptr, nullptr, 1);
@@ -510,7 +525,7 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
                                                     smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
-  DTG_TPR_SWITCH(g.tpr, bn_apply2_kernel<T><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa));
+  DTG_TPR_SWITCH(g.tpr, bn_apply2_kernel<T><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa, bits));
 }
 
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.

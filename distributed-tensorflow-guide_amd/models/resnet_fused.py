@@ -60,10 +60,11 @@ _LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction 
 
 class _Bn3Link:
     """Block i's BN3 tensors, filled with the mode-3 partials by block i+1's backward."""
-    __slots__ = ("y3", "m3", "i3", "gamma", "beta", "part", "dp")
+    __slots__ = ("y3", "m3", "i3", "gamma", "beta", "bits", "part", "dp")
 
-    def __init__(self, y3, m3, i3, gamma, beta):
+    def __init__(self, y3, m3, i3, gamma, beta, bits):
         self.y3, self.m3, self.i3, self.gamma, self.beta = y3, m3, i3, gamma, beta
+        self.bits = bits  # packed (out > 0): the relu mask, 1/16 of the bytes of re-reading out
         self.part = self.dp = None
 
 
@@ -122,20 +123,23 @@ class _BottleneckFn(torch.autograd.Function):
                                               bd.momentum, bd.eps, False)
         else:
             idn = x2
+        bits = None
+        if _FUSE and _LINK:
+            bits = torch.empty(y3.shape[0], cout // 8, device=y3.device, dtype=torch.uint8)
         if _FUSE and blk.down is not None:  # out = relu(bn3(y3) + bn_d(yd)) in one pass
             assert bd.momentum == b3.momentum and bd.eps == b3.eps
             out, m3, i3, md, idd = L.bn_fwd2_part(y3, p3, b3.weight, b3.bias, b3.running_mean, b3.running_var, yd, pd,
                                                   bd.weight, bd.bias, bd.running_mean, bd.running_var, b3.momentum,
-                                                  b3.eps)
+                                                  b3.eps, bits=bits)
         elif _FUSE:
             out, m3, i3 = L.bn_fwd_part(y3, p3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var,
-                                        b3.momentum, b3.eps, True)
+                                        b3.momentum, b3.eps, True, bits=bits)
         else:
             out, m3, i3 = L.bn_fwd_train(y3, idn, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.momentum,
                                          b3.eps, True)
         ctx.blk = blk
         ctx.link_in = link_in if (_FUSE and _LINK) else None
-        ctx.link_out = _Bn3Link(y3, m3, i3, b3.weight, b3.bias) if (_FUSE and _LINK) else None
+        ctx.link_out = _Bn3Link(y3, m3, i3, b3.weight, b3.bias, bits) if (_FUSE and _LINK) else None
         holder.append(ctx.link_out)
         ctx.geom = (n, c, h, w, st, width, cout, p_, q_)
         ctx.save_for_backward(x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3,
@@ -224,7 +228,7 @@ class _BottleneckFn(torch.autograd.Function):
         if not dx_done:
             if lk_in is not None:  # mode 3: finish the previous block's BN3 reduction in this epilogue
                 _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                    mask=x2, out=dx2, pooled=True)
+                                    mask=lk_in.bits, out=dx2, pooled=True)
                 lk_in.part, lk_in.dp = part, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)

@@ -160,3 +160,38 @@ def test_bn_fwd2_part_matches_two_passes():
         outs.append((o, m3, i3, md, idd, rm3, rv3, rmd, rvd))
     for x, y in zip(outs[1], outs[0]):
         assert _rel(x, y) < 1e-2
+
+
+def _pack_bits(t):
+    b = (t.float() > 0).to(torch.uint8).view(t.shape[0], -1, 8)
+    w = (1 << torch.arange(8, device=t.device, dtype=torch.int32)).to(torch.uint8)
+    return (b * w).sum(-1).to(torch.uint8)
+
+
+def test_mode3_packed_mask_bits():
+    """bn_fwd_part emits the packed relu mask of its output; gemm_bn mode 3 gives identical results with
+    the packed mask and with the bf16 tensor it was packed from (and accumulates into `out`)."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, K, N = 1536, 128, 256
+    L = lib()
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    y, part = L.gemm_bn(a, w, 1)
+    res = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    gamma, beta = (torch.rand(N, generator=g) + 0.5).to(dev), (torch.randn(N, generator=g) * 0.1).to(dev)
+    bits = torch.empty(M, N // 8, device=dev, dtype=torch.uint8)
+    out, m, i = L.bn_fwd_part(y, part, res, gamma, beta, torch.zeros(N, device=dev), torch.ones(N, device=dev), 0.1,
+                              1e-5, True, bits=bits)
+    assert torch.equal(bits, _pack_bits(out))
+    dy = torch.randn(M, 64, generator=g).to(dev, torch.bfloat16)
+    w1 = torch.randn(64, N, generator=g).mul_(0.125).to(dev, torch.bfloat16)
+    acc0 = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    r = []
+    for mask in (out, bits):
+        o = acc0.clone()
+        dp, q = L.gemm_bn(dy, w1, 3, y, m, i, gamma, beta, mask=mask, out=o)
+        r.append((o, q))
+    assert torch.equal(r[0][0], r[1][0]) and torch.allclose(r[0][1], r[1][1], rtol=1e-4, atol=1e-3)
+    ref = torch.where(out.float() > 0, dy.float() @ w1.float() + acc0.float(), torch.zeros(M, N, device=dev))
+    assert _rel(r[1][0], ref) < 1e-2
