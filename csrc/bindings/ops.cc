@@ -356,6 +356,34 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   return dx;
 }
 
+// 8-channel input conv (the stem): x [N,H,W,8] NHWC, w [K, Kp] with Kp = ceil64(R*S*8), (r,s,c) columns.
+// with_stats: also the forward BN statistics of y (returned partials, else an empty tensor).
+std::tuple<Tensor, Tensor> conv_fwd_c8(Tensor x, Tensor w, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                                       bool with_stats) {
+  check_nhwc(x, "x");
+  CHECK_IN(w);
+  CHECK_DT(w, at::kBFloat16);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), K = w.size(0);
+  TORCH_CHECK(x.size(3) == 8, "conv_fwd_c8 needs 8 input channels");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == (R * S * 8 + 63) / 64 * 64, "w must be [K, ceil64(R*S*8)]");
+  TORCH_CHECK(K % 64 == 0, "K % 64");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0 && (long long)N * P * Q * K < (1LL << 31), "bad geometry");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, P, Q, K}, x.options());
+  Tensor part;
+  dtg::BnEpi bn;
+  if (with_stats) {
+    part = at::zeros({(long long)dtg::kBnStatSlots * 2 * K}, x.options().dtype(at::kFloat));
+    bn.part = part.data_ptr<float>();
+    bn.mode = 1;
+  } else {
+    part = at::empty({0}, x.options().dtype(at::kFloat));
+  }
+  dtg::conv_fwd_c8(cbfp(x), cbfp(w), bfp(y), N, H, W, K, (int)R, (int)S, (int)stride, (int)pad, cur_stream(), bn);
+  return {y, part};
+}
+
 // ---- BN statistics fused into the producing GEMM / conv (dtg/bn_epi.cuh) ----------------------
 // Statistics slots.  pooled: a buffer from a per-device ring of zeroed buffers which the consuming
 // finalize (bn_*_part) zeroes again after reading -- no fill kernel per BN.  The caller must consume
@@ -665,6 +693,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("r"), pybind11::arg("part2"),
         pybind11::arg("gamma2"), pybind11::arg("beta2"), pybind11::arg("rmean2"), pybind11::arg("rvar2"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("bits") = pybind11::none());
+  m.def("conv_fwd_c8", &conv_fwd_c8, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("R"), pybind11::arg("S"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("with_stats") = false);
   m.def("bn_fwd_part", &bn_fwd_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("res"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("bits") = pybind11::none());

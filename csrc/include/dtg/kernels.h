@@ -150,6 +150,8 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
 // with residue classes no tap reaches)
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
                int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi());
+void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
+                 int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad);
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,

@@ -42,7 +42,10 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
 }
 
 // ---- fwd A: x gathered at the output positions of the tile rows (KC) ---------------------------
-template <int ROWS>
+// C8: the input has exactly 8 (zero-padded) channels -- the ResNet stem, 3 -> 8 -- so one 16-B
+// chunk is one pixel and a 64-deep K step spans 8 (r, s) taps; K runs over (r, s, c) padded to a
+// multiple of 64 (taps rs >= R*S read the zero page; their weights are zero too).
+template <int ROWS, bool C8 = false>
 struct FwdA {
   static constexpr int PW = ROWS / 32;
   const bf16_t* x;
@@ -68,13 +71,21 @@ struct FwdA {
   }
   __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave) const {
     uint32_t rs, c0, r, s;
-    g->fC.divmod((uint32_t)k0, rs, c0);
-    g->fS.divmod(rs, r, s);
-    const int ch = (int)c0 + cx * 8;
+    bool rs_ok = true;
+    if constexpr (C8) {
+      rs = (uint32_t)(k0 >> 3) + cx;
+      c0 = 0;
+      rs_ok = rs < (uint32_t)(g->R * g->S);
+      g->fS.divmod(rs_ok ? rs : 0, r, s);
+    } else {
+      g->fC.divmod((uint32_t)k0, rs, c0);
+      g->fS.divmod(rs, r, s);
+    }
+    const int ch = C8 ? 0 : (int)c0 + cx * 8;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int ih = ih0[i] + (int)r, iw = iw0[i] + (int)s;
-      const bool ok = (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
+      const bool ok = rs_ok && (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
       const int ihc = ok ? ih : 0, iwc = ok ? iw : 0;
       const void* src = sel(ok, x + ((long long)(nbase[i] + ihc) * g->W + iwc) * g->C + ch);
       const int r0 = (wave * PW + i) * 8;
@@ -265,7 +276,7 @@ struct DgradSB {
 };
 
 // ---------------------------------------------------------------------------------------------
-template <class CF, int BNMODE = 0>
+template <class CF, int BNMODE = 0, bool C8 = false>
 __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
@@ -274,8 +285,8 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int M = G.N * G.P * G.Q, Kd = G.R * G.S * G.C;
-  FwdA<CF::BM> sa;
+  const int M = G.N * G.P * G.Q, Kd = C8 ? (G.R * G.S * 8 + 63) / 64 * 64 : G.R * G.S * G.C;  // C8: w is [K][Kd]
+  FwdA<CF::BM, C8> sa;
   sa.init(G, x, bm0, wave, lane);
   DenseKC<false> sb{w, (long long)Kd, G.K, Kd};
   f32x4 acc[4][4];
@@ -409,6 +420,7 @@ void conv_set_stages(int which, int stages) {  // 0 restores the measured defaul
 }
 
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
+  if (C == 8 && K % 64 == 0 && which != 1) return 1;  // stem: fwd (conv_fwd_c8) and wgrad
   if (C % 64 || K % 64) return 0;
   if (which == 1 && stride * stride > kMaxClasses) return 0;  // one launch holds <= 9 residue classes
   return 1;
@@ -428,6 +440,22 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   const bool s1 = conv_stages(0, M, K, R * S * C) == 1;
   if (conv_skinny(K)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
   else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+}
+
+// 8-channel input (the stem, zero padded 3 -> 8); w is [K][Kp], Kp = ceil64(R*S*8), (r, s, c) order
+void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
+                 int pad, hipStream_t st, const BnEpi& bn) {
+  ConvGeom G = make_geom(N, H, W, 8, K, R, S, stride, pad);
+  const int M = N * G.P * G.Q;
+  Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
+  auto run = [&](auto cf) {
+    using CF = decltype(cf);
+    const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    if (bn.mode == 1) conv_fwd_kernel<CF, 1, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
+    else conv_fwd_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
+  };
+  if (conv_skinny(K)) run(Cfg<256, 64, 1>());
+  else run(Cfg<128, 128, 1>());
 }
 
 static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,

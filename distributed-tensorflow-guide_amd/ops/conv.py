@@ -8,7 +8,10 @@ Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
   * small channel counts (C % 64 != 0, K % 8 == 0: MNIST's 1/32-channel convs) -> im2col kernel +
     MFMA GEMM with the bias/ReLU epilogue; dgrad = GEMM + col2im gather kernel
     (``conv2d_bias_act``)
-  * everything else (the 7x7/Cin=3 stem) -> MIOpen through torch
+  * <= 8 input channels with K % 64 == 0 (the 7x7/2 Cin=3 stem) -> implicit-GEMM conv on the input
+    zero-padded to 8 channels (one pixel = one 16-B chunk, csrc/kernels/conv.hip ``conv_fwd_c8``) and
+    the same kernel's wgrad; no dgrad (the stem's input is the image)
+  * everything else -> MIOpen through torch
 Weight gradients are accumulated straight into the flat gradient buffer (see parallel/grad_sink).
 """
 import os
@@ -104,6 +107,41 @@ class _ConvImplicit(torch.autograd.Function):
         return dx, dw4.permute(0, 3, 1, 2), None, None
 
 
+class _ConvC8(torch.autograd.Function):
+    """Few-channel input conv (ResNet stem): input padded to 8 channels, weights to [K, ceil64(R*S*8)]."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        n, c, h, wd = x.shape
+        k, _, r, s = w.shape
+        x8 = F.pad(_nhwc(x), (0, 8 - c)).contiguous()          # [N, H, W, 8]
+        w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
+        kp = (r * s * 8 + 63) // 64 * 64
+        w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()       # [K, Kp], (r, s, c) columns
+        y4, _ = lib().conv_fwd_c8(x8, w8, r, s, stride, pad)
+        ctx.save_for_backward(x8)
+        ctx.geom = (c, k, r, s, stride, pad)
+        ctx.param = w if grad_sink.enabled(w) else None
+        ctx.needs_dx = ctx.needs_input_grad[0]
+        return y4.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x8,) = ctx.saved_tensors
+        c, k, r, s, st, pad = ctx.geom
+        if ctx.needs_dx:
+            raise NotImplementedError("input gradient of the 8-channel stem conv (the image needs none)")
+        dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
+        lib().conv_wgrad(_nhwc(dy).contiguous(), x8, dw8, 0.0, st, pad)
+        dw = dw8[..., :c].permute(0, 3, 1, 2)                    # [K, C, R, S] view
+        p = ctx.param
+        if p is not None:
+            p.grad.add_(dw.to(p.grad.dtype))
+            grad_sink.notify(p)
+            return None, None, None, None
+        return None, dw.to(ctx.saved_tensors[0].dtype).contiguous(memory_format=torch.channels_last), None, None
+
+
 def _kp(w):
     return (w.shape[1] * w.shape[2] * w.shape[3] + 7) // 8 * 8
 
@@ -169,4 +207,6 @@ def conv2d(x, w, stride=1, padding=0):
             return _Conv1x1.apply(x, w)
         if cin % 64 == 0 and cout % 64 == 0:
             return _ConvImplicit.apply(x, w, stride, padding)
+        if cin <= 8 and cout % 64 == 0 and not x.requires_grad:
+            return _ConvC8.apply(x, w, stride, padding)
     return F.conv2d(x, w, None, stride, padding)

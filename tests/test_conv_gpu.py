@@ -85,3 +85,22 @@ def test_conv_dgrad_strided_accumulate(R, st, pad, H):
     assert _rel(out, base.float() + ref) < 1e-2
     fresh = lib().conv_dgrad(dy, w, H, H, st, pad)
     assert _rel(fresh, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,K,H,R,st,pad", [(2, 3, 64, 32, 7, 2, 3), (2, 3, 64, 23, 7, 2, 3), (3, 4, 128, 16, 3, 1, 1)])
+def test_conv_c8_stem(N, C, K, H, R, st, pad):
+    """Few-channel input (the ResNet stem): input padded to 8 channels, implicit-GEMM fwd + wgrad."""
+    from dtg.ops.conv import _ConvC8
+    g = torch.Generator(device="cpu").manual_seed(7 + H)
+    x = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, generator=g) * (2.0 / (C * R * R)) ** 0.5).to(DEV, torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = ops.conv2d(x, w, st, pad)
+    assert "ConvC8" in type(y.grad_fn).__name__
+    wr = w.detach().float().requires_grad_()
+    yr = F.conv2d(x.float(), wr, None, st, pad)
+    assert y.shape == yr.shape and _rel(y, yr) < 1e-2
+    gy = torch.randn(yr.shape, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(gy)
+    yr.backward(gy.float())
+    assert _rel(w.grad, wr.grad) < 2e-2
