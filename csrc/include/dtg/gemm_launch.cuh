@@ -26,10 +26,21 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
     if (e.aux) e.aux = (char*)e.aux + co * 2;
   }
   const int ntiles = gridDim.x;  // tiles per split
-  const int t = xcd_remap(blockIdx.x, ntiles);
+  // XCD-aware over the whole (tile, split) grid: the hardware deals linear workgroup ids round-robin
+  // to the 8 XCDs, so remapping blockIdx.x alone would scatter the tiles of one K-split (which share
+  // their A/B K-slabs) over all 8 L2s.  Remapped, consecutive (split, tile) work ids -- all tiles of a
+  // split -- land on one XCD and re-read the slabs from its L2.
+  int t, split;
+  if (gridDim.y > 1) {
+    const int w = xcd_remap(blockIdx.x + blockIdx.y * ntiles, ntiles * gridDim.y);
+    split = w / ntiles;
+    t = w - split * ntiles;
+  } else {
+    t = xcd_remap(blockIdx.x, ntiles);
+    split = 0;
+  }
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int bm0 = tm * CF::BM, bn0 = tn * CF::BN;
-  const int split = blockIdx.y;
   const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
   f32x4 acc[4][4];

@@ -338,12 +338,15 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
   lds_char* smem = (lds_char*)smem_raw;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  // (split, tile) remapped over the whole grid so a K-split's tiles share one XCD's L2 (see gemm_kernel)
+  const int ntl = gridDim.x;
+  const int wid = xcd_remap(blockIdx.x + blockIdx.y * ntl, ntl * gridDim.y);
+  const int split = wid / ntl, t = wid - split * ntl;
   const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = G.N * G.P * G.Q;              // reduction length
   const int Mo = G.K, No = G.R * G.S * G.C;   // output dw [K][RSC]
-  const int kbeg = blockIdx.y * k_per_split, kend = min(M, kbeg + k_per_split);
+  const int kbeg = split * k_per_split, kend = min(M, kbeg + k_per_split);
   DenseMC<true> sa{dy, (long long)G.K, G.K, M};
   WgradB<CF::BN> sb{x, &G, bn0, M};
   f32x4 acc[4][4];
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop_st<CF, false, false>([&](lds_char* tl, int k0) { stage_mc<CF::BM>(sa, tl, bm0, k0, wave, lane); },
                                 [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, kbeg, kend, acc);
-  float* slab = ws + (long long)blockIdx.y * Mo * No;
+  float* slab = ws + (long long)split * Mo * No;
   epilogue_staged<CF>(smem, acc, bm0, bn0, Mo, No, [&](int m, int n, float (&v)[8]) {
     store8_f32(slab + (long long)m * No + n, v);
   });
