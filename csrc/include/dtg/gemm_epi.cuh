@@ -16,22 +16,27 @@ struct Epi {
   int aux_mode = 0;     // 0 none; 1 store the pre-activation to aux; 2 multiply by act'(aux) (act backward)
 };
 
+// GELU (tanh form) through its sigmoid identity 0.5 * (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 and
+// one v_rcp_f32 instead of libm tanhf (range reduction and branches), which made the GELU GEMM
+// epilogues issue-bound.  exp overflow is benign: sigmoid -> 0 or 1.
+__device__ __forceinline__ float gelu_sig(float x) {  // sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3)
+  const float u2 = 1.5957691216057308f * fmaf(0.044715f * x, x * x, x);
+  return __builtin_amdgcn_rcpf(1.f + __expf(-u2));
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
-  if (act == 2) {
-    const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
-    return 0.5f * v * (1.f + tanhf(u));
-  }
+  if (act == 2) return v * gelu_sig(v);
   return v;
 }
 
-// d act(x) / dx
+// d act(x) / dx;  GELU: s + x * (1 - t^2)/2 * u' with t = 2s - 1, (1 - t^2) = 4 s (1 - s)
 __device__ __forceinline__ float act_grad(float x, int act) {
   if (act == 1) return x > 0.f ? 1.f : 0.f;
   if (act == 2) {
-    const float k = 0.7978845608028654f;
-    const float t = tanhf(k * (x + 0.044715f * x * x * x));
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+    const float s = gelu_sig(x);
+    const float du = 0.7978845608028654f * fmaf(3.f * 0.044715f * x, x, 1.f);
+    return fmaf(2.f * x * s * (1.f - s), du, s);
   }
   return 1.f;
 }
@@ -98,6 +103,42 @@ __device__ __forceinline__ void epi_store8_fast(const Epi& e, int m, int n, floa
   } else if (e.alpha != 1.f) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+  }
+  store8_bf16(p, v);
+}
+
+// epi_store8_fast plus bias / activation / aux (bf16, full aligned groups): the switches are
+// wave-uniform branches around whole 8-column loops, not per-element tests as in epi_store8.
+__device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, float (&v)[8]) {
+  const long long off = (long long)m * e.ldc + n;
+  bf16_t* p = (bf16_t*)e.C + off;
+  if (e.beta != 0.f) {
+    float old[8];
+    load8_bf16(p, old);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], e.alpha, e.beta * old[k]);
+  } else if (e.alpha != 1.f) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+  }
+  if (e.bias) {
+    float b[8];
+    load8_f32(e.bias + n, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += b[k];
+  }
+  if (e.aux_mode == 1) store8_bf16((bf16_t*)e.aux + off, v);
+  if (e.aux_mode == 2) {
+    float pre[8];
+    load8_bf16((const bf16_t*)e.aux + off, pre);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= act_grad(pre[k], e.act);
+  } else if (e.act == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+  } else if (e.act == 2) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= gelu_sig(v[k]);
   }
   store8_bf16(p, v);
 }

@@ -64,18 +64,24 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
     });
     return;
   }
-  if constexpr (FAST) {  // bf16, aligned, no bias/act/aux (fast_epi() checked): no per-group switches
-    auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); };
-    epilogue_staged<CF, decltype(op), !SA::kGuard && !SB::kGuard>(smem, acc, bm0, bn0, M, N, op);
+  if constexpr (FAST) {  // bf16, aligned (fast_epi() checked): no per-group / per-element switches
+    constexpr bool FULL = !SA::kGuard && !SB::kGuard;
+    if (!e.bias && e.act == 0 && e.aux_mode == 0) {
+      auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); };
+      epilogue_staged<CF, decltype(op), FULL>(smem, acc, bm0, bn0, M, N, op);
+    } else {
+      auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast_act(e, m, n, v); };
+      epilogue_staged<CF, decltype(op), FULL>(smem, acc, bm0, bn0, M, N, op);
+    }
   } else {
     epilogue_staged<CF>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) { epi_store8(e, N, m, n, v); });
   }
 }
 
-// epilogue specialisation: bf16 output, 16-B aligned 8-column groups, no bias / activation / aux
+// epilogue specialisation: bf16 output (and aux), 16-B aligned 8-column groups
 inline bool fast_epi(const Epi& e, int N) {
-  return e.c_bf16 && !e.bias && e.act == 0 && e.aux_mode == 0 && (e.ldc % 8) == 0 && (N % 8) == 0 &&
-         ((uintptr_t)e.C % 16) == 0;
+  return e.c_bf16 && (e.ldc % 8) == 0 && (N % 8) == 0 && ((uintptr_t)e.C % 16) == 0 &&
+         ((uintptr_t)e.bias % 16) == 0 && ((uintptr_t)e.aux % 16) == 0;
 }
 
 template <class CF, bool AK, bool BK_, bool GUARD>

@@ -161,29 +161,45 @@ struct DgradB {
 };
 
 // ---- wgrad B: x as B[(n,p,q)][(r,s,c)] (MC: c contiguous) ----------------------------------------
+// A lane's columns (r, s, c) are the same at every K step (k0 advances by 64 rows and the MC swizzle
+// depends on the row within the tile only), so they are decomposed once in init(); a K step
+// decomposes only its rows m = k0 + kr into (n, p, q).
 template <int ROWS>
 struct WgradB {
   static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
   const bf16_t* x;
   const ConvGeom* g;
-  int col0, M;
+  int M;
+  int dr[PW], ds[PW], cc[PW];  // r - pad, s - pad, channel; a padded column gets dr far out of range
+  __device__ __forceinline__ void init(const bf16_t* xp, const ConvGeom& G, int col0, int Mrows, int wave, int lane) {
+    x = xp;
+    g = &G;
+    M = Mrows;
+    const int ncols = G.R * G.S * G.C;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int kr = (wave * PW + i) * KPI + lane / CH;
+      const int c = (lane % CH) ^ mc_swz<CH>(kr);
+      const int col = col0 + c * 8;
+      uint32_t rs, ch, r, s;
+      G.fC.divmod((uint32_t)(col < ncols ? col : 0), rs, ch);
+      G.fS.divmod(rs, r, s);
+      dr[i] = col < ncols ? (int)r - G.pad : -(1 << 28);
+      ds[i] = (int)s - G.pad;
+      cc[i] = (int)ch;
+    }
+  }
   __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave, int lane) const {
-    const int ncols = g->R * g->S * g->C;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int kr0 = (wave * PW + i) * KPI;
-      const int kr = kr0 + lane / CH;
-      const int c = (lane % CH) ^ mc_swz<CH>(kr);
-      const int col = col0 + c * 8;
-      const int m = k0 + kr;
-      uint32_t n, pq, p, q, rs, cc, r, s;
+      const int m = k0 + kr0 + lane / CH;
+      uint32_t n, pq, p, q;
       g->fPQ.divmod((uint32_t)(m < M ? m : 0), n, pq);
       g->fQ.divmod(pq, p, q);
-      g->fC.divmod((uint32_t)(col < ncols ? col : 0), rs, cc);
-      g->fS.divmod(rs, r, s);
-      const int ih = (int)p * g->stride - g->pad + (int)r, iw = (int)q * g->stride - g->pad + (int)s;
-      const bool ok = m < M && col < ncols && (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
-      const void* src = sel(ok, x + ((long long)((int)n * g->H + (ok ? ih : 0)) * g->W + (ok ? iw : 0)) * g->C + cc);
+      const int ih = (int)p * g->stride + dr[i], iw = (int)q * g->stride + ds[i];
+      const bool ok = m < M && (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
+      const void* src = sel(ok, x + ((long long)((int)n * g->H + (ok ? ih : 0)) * g->W + (ok ? iw : 0)) * g->C + cc[i]);
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + kr0 * ROWS * 2), 16, 0, 0);
     }
   }
@@ -348,7 +364,8 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   const int Mo = G.K, No = G.R * G.S * G.C;   // output dw [K][RSC]
   const int kbeg = split * k_per_split, kend = min(M, kbeg + k_per_split);
   DenseMC<true> sa{dy, (long long)G.K, G.K, M};
-  WgradB<CF::BN> sb{x, &G, bn0, M};
+  WgradB<CF::BN> sb;
+  sb.init(x, G, bn0, M, wave, lane);
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
