@@ -210,7 +210,14 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
     return;
   }
-  if (short_m(M, N)) {  // 64-row weight gradients (64-channel layers): no half-empty 128-row tiles
+  if (split_k > 1 || !a_kc) {
+    // weight gradients (MN-contiguous A, split-K over the token/pixel dimension): the single-stage
+    // 128x128 ring beat every other tile and the 2-stage ring on all of them, BERT's 768x3072x8192
+    // by 1.4x (profiles/r01_tiles/sweep_wgrad.json)
+    launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    return;
+  }
+  if (short_m(M, N)) {  // 64-row outputs: no half-empty 128-row tiles
     launch_cfg<64, 256>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
     return;
   }
@@ -223,10 +230,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
   // (< 512 tiles) and K long enough (>= 2048) that in-block prefetch pays (profiles/r01_tiles).
   const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * split_k * bt.count;
-  if (split_k > 1 || !a_kc) {  // split-K weight gradients: tile/ring choice measured flat (r01_tiles)
-    if (skinny(N)) launch_cfg<256, 64>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-    else launch_cfg<128, 128>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  } else if (tiles128 < 512 && kps >= 2048) {
+  if (tiles128 < 512 && kps >= 2048) {
     launch_exact<Cfg<128, 128, 2>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else if (skinny(N)) {
     launch_exact<Cfg<256, 64, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);

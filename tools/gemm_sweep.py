@@ -37,6 +37,9 @@ SHAPES = [
     (64, 256, 802816, False, False, 1.0), (256, 64, 802816, False, False, 1.0), (128, 512, 200704, False, False, 1.0),
     (512, 128, 200704, False, False, 1.0), (256, 1024, 50176, False, False, 1.0), (1024, 256, 50176, False, False, 1.0),
     (2048, 512, 12544, False, False, 1.0),
+    # BERT-base weight gradients (tokens = 64 x 128)
+    (768, 3072, 8192, False, False, 1.0), (3072, 768, 8192, False, False, 1.0), (2304, 768, 8192, False, False, 1.0),
+    (768, 768, 8192, False, False, 1.0),
 ]
 
 
@@ -58,16 +61,17 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--cfgs", default="0,1,2,3,14,15,16,17,18,19,20,21,22,23,24")
     ap.add_argument("--shapes", default="", help="comma list of shape indices (default all)")
+    ap.add_argument("--splits", default="", help="comma list of split-K counts to force (0 = auto)")
     a = ap.parse_args()
     L = lib()
     cfgs = [int(c) for c in a.cfgs.split(",")]
     res = []
     idx = [int(i) for i in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
     for (M, N, K, akc, bkc, beta) in [SHAPES[i] for i in idx]:
-        split = 0 if K >= 8192 else 1  # wgrad shapes: the binding's automatic split-K
+        splits = [int(v) for v in a.splits.split(",")] if a.splits else [0 if K >= 8192 else 1]
         A = torch.randn((M, K) if akc else (K, M), device="cuda", dtype=torch.bfloat16)
         B = torch.randn((N, K) if bkc else (K, N), device="cuda", dtype=torch.bfloat16)
-        C = torch.randn(M, N, device="cuda", dtype=torch.float32 if split == 0 else torch.bfloat16)
+        C = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
         ref = None
         by = (A.numel() + B.numel()) * 2 + C.numel() * 2 * (2 if beta else 1)
         fl = 2.0 * M * N * K
@@ -75,22 +79,24 @@ def main():
         for c in cfgs:
             if c in (5, 6, 7, 14, 20, 22) and N > 64 and N % 64:
                 continue
-            L.gemm_force_cfg(c)
-            out = torch.zeros_like(C)
-            L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, split)
-            if ref is None:
-                ref = out.float()
-            err = ((out.float() - ref).norm() / (ref.norm() + 1e-9)).item()
-            us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, split))
-            rows.append((c, us, err))
+            for split in splits:
+                L.gemm_force_cfg(c)
+                out = torch.zeros_like(C)
+                L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, split)
+                if ref is None:
+                    ref = out.float()
+                err = ((out.float() - ref).norm() / (ref.norm() + 1e-9)).item()
+                us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, split))
+                rows.append((c if len(splits) == 1 else (c, split), us, err))
         L.gemm_force_cfg(0)
         best = min(r[1] for r in rows)
         for c, us, err in rows:
             mark = " *" if us == best else ""
+            name = NAMES[c] if isinstance(c, int) else f"{NAMES[c[0]]}/split{c[1]}"
             print(f"{M:7d}x{N:5d}x{K:5d} {'KC' if akc else 'MC'}{'KC' if bkc else 'MC'} b={beta:.0f} "
-                  f"{NAMES[c]:12s} {us:8.1f} us {by / us / 1e6:5.2f} TB/s {fl / us / 1e6:6.1f} TF/s err={err:.1e}{mark}",
+                  f"{name:18s} {us:8.1f} us {by / us / 1e6:5.2f} TB/s {fl / us / 1e6:6.1f} TF/s err={err:.1e}{mark}",
                   flush=True)
-            res.append({"M": M, "N": N, "K": K, "akc": akc, "bkc": bkc, "beta": beta, "cfg": NAMES[c], "us": us,
+            res.append({"M": M, "N": N, "K": K, "akc": akc, "bkc": bkc, "beta": beta, "cfg": name, "us": us,
                         "err": err})
         del A, B, C
     if a.json:
