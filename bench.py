@@ -31,7 +31,10 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default 256 resnet / 64 bert)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--bucket_mb", type=float, default=32.0)
+    # all-reduce bucket size: ResNet-50's 51 MB of bf16 gradients in 8 MB buckets (backward order) leaves
+    # only the last ~3 MB (layer2/layer1/stem) exposed after backward ends; 32 MB buckets would leave
+    # ~20 MB (layer3 onwards) to reduce after the last gradient lands.  BERT (220 MB) uses 25 MB.
+    ap.add_argument("--bucket_mb", type=float, default=0.0, help="0: 8 (resnet50) / 25 (bert)")
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--model", default="resnet50")
     return ap.parse_known_args(argv)[0]
@@ -47,6 +50,7 @@ def main(argv=None):
     from dtg import ops
 
     rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
+    a.bucket_mb = a.bucket_mb or (25.0 if a.model == "bert" else 8.0)
     if world != a.gpus and rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.manual_seed(1234)
