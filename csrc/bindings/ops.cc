@@ -332,6 +332,13 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad) {
   return y;
 }
 
+// DTG_DGRAD_WT=1: stride-1 dgrad reads the weight transposed to [C][(r,s,k)] (K-contiguous) instead of
+// the MN-contiguous image; measured equal within +-5 % on the ResNet-50 3x3 layers (off by default)
+static bool dgrad_wt() {
+  static const bool on = getenv("DTG_DGRAD_WT") && getenv("DTG_DGRAD_WT")[0] == '1';
+  return on;
+}
+
 // dx (= or +=, beta) dgrad; `out` (optional, [N,H,W,C] bf16) receives it in place
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, c10::optional<Tensor> out,
                   double beta) {
@@ -352,7 +359,9 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     TORCH_CHECK(beta == 0.0, "beta != 0 needs out");
     dx = at::empty({N, H, W, C}, dy.options());
   }
-  dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, (float)beta, cur_stream());
+  Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();  // see conv_dgrad_bn
+  dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, (float)beta, cur_stream(),
+                  dtg::BnEpi(), wT.defined() ? cbfp(wT) : nullptr);
   return dx;
 }
 
@@ -516,7 +525,10 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t
   auto dx = at::empty({N, H, W, C}, dy.options());
   auto part = bn_part(dy, C, pooled);
   dtg::BnEpi bn = bn_bwd_epi(part, x, mean, invstd, gamma, beta, (long long)N * H * W, C);
-  TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn),
+  // stride 1: the kernel reads the weight transposed to [C][(r,s,k)] (K-contiguous; ~1 MB, one small copy)
+  Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();
+  TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn,
+                              wT.defined() ? cbfp(wT) : nullptr),
               "conv_dgrad_bn: geometry leaves rows unwritten (use conv_dgrad + bn_bwd)");
   return {dx, part};
 }

@@ -148,8 +148,10 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
               int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 // returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad
 // with residue classes no tap reaches)
+// wT (optional): the weight transposed to [C][(r,s,k)] (K-contiguous), used by the stride-1 kernels
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi());
+               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi(),
+               const bf16_t* wT = nullptr);
 void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
                  int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad

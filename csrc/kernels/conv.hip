@@ -320,7 +320,10 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
   epilogue_staged<CF>(smem, acc, bm0, bn0, M, G.K, [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); });
 }
 
-template <class CF, int BNMODE = 0>
+// WT: w is the transposed weight wT[c][(r,s,k)] (K-contiguous, transposed once per step by the caller),
+// so B is staged like the forward's weights (ds_read_b128) instead of through the MN-contiguous
+// [(r,s,k)][c] image and hardware-transposed reads
+template <class CF, int BNMODE = 0, bool WT = false>
 __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
@@ -332,14 +335,21 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
   const int M = G.N * G.H * G.W, Kd = G.R * G.S * G.K;
   DgradA<CF::BM> sa;
   sa.init(G, dy, bm0, wave, lane);
-  DgradB<CF::BN> sb{w, &G, bn0};
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
-                               [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
+  if constexpr (WT) {
+    DenseKC<true> sb{w, (long long)Kd, G.C, Kd};
+    mainloop_st<CF, true, true>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
+                                [&](lds_char* tl, int k0) { stage_kc<CF::BN>(sb, tl, bn0, k0, wave, lane); }, smem,
+                                0, Kd, acc);
+  } else {
+    DgradB<CF::BN> sb{w, &G, bn0};
+    mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
+                                 [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
+  }
   if constexpr (BNMODE != 0) {
     epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.C, e, bn, t, [](int m) { return m; });
     return;
@@ -534,7 +544,7 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
 }
 
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn) {
+               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn, const bf16_t* wT) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st, bn);
   const int M = N * H * W;
@@ -545,7 +555,18 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
     if (bn.mode == 2) conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
     else conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
   };
+  auto run_t = [&](auto cf) {  // K-contiguous transposed weights
+    using CF = decltype(cf);
+    const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
+    if (bn.mode == 2) conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
+    else conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
+  };
   const bool s1 = conv_stages(1, M, C, R * S * K) == 1;
+  if (wT && s1) {
+    if (conv_skinny(C)) run_t(Cfg<256, 64, 1>());
+    else run_t(Cfg<128, 128, 1>());
+    return 1;
+  }
   if (conv_skinny(C)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
   else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
   return 1;
