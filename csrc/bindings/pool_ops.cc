@@ -26,6 +26,7 @@ void check_nhwc8(const Tensor& t, const char* what) {
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   check_nhwc8(x, "x");
   TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && pad >= 0 && pad < k, "unsupported pooling window");
+  TORCH_CHECK(x.numel() / 8 < (1LL << 31), "max-pool kernels index 16-byte vectors with 32-bit math");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
   TORCH_CHECK(P > 0 && Q > 0, "empty output");
@@ -42,6 +43,7 @@ Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64
               "idx must be uint8 shaped like dy");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
   TORCH_CHECK((H + 2 * pad - k) / s + 1 == P && (W + 2 * pad - k) / s + 1 == Q, "pool geometry mismatch");
+  TORCH_CHECK((long long)N * H * W * (C / 8) < (1LL << 31), "max-pool kernels index 16-byte vectors with 32-bit math");
   c10::DeviceGuard dg(dy.device());
   auto dx = at::empty({N, H, W, C}, dy.options());
   dtg::maxpool_bwd(cbfp(dy), idx.data_ptr<uint8_t>(), bfp(dx), N, (int)H, (int)W, C, k, s, pad, P, Q, cur_stream());

@@ -16,16 +16,15 @@ struct PoolGeom {
 
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeom g) {
-  const int c8n = g.C >> 3;
-  const long long total = (long long)g.N * g.P * g.Q * c8n;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  const unsigned c8n = g.C >> 3;
+  const unsigned total = (unsigned)g.N * g.P * g.Q * c8n;  // < 2^31 (host check): 32-bit index math
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c8 = (int)(i % c8n);
-    long long t = i / c8n;
-    const int q = (int)(t % g.Q);
-    t /= g.Q;
-    const int p = (int)(t % g.P);
-    const int n = (int)(t / g.P);
+    unsigned t = i / c8n;
+    const int q = (int)(t % (unsigned)g.Q);
+    t /= (unsigned)g.Q;
+    const int p = (int)(t % (unsigned)g.P);
+    const int n = (int)(t / (unsigned)g.P);
     float m[8];
     uint8_t am[8];
 #pragma unroll
@@ -65,16 +64,15 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
                                                           PoolGeom g) {
-  const int c8n = g.C >> 3;
-  const long long total = (long long)g.N * g.H * g.W * c8n;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  const unsigned c8n = g.C >> 3;
+  const unsigned total = (unsigned)g.N * g.H * g.W * c8n;  // < 2^31 (host check): 32-bit index math
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c8 = (int)(i % c8n);
-    long long t = i / c8n;
-    const int w = (int)(t % g.W);
-    t /= g.W;
-    const int h = (int)(t % g.H);
-    const int n = (int)(t / g.H);
+    unsigned t = i / c8n;
+    const int w = (int)(t % (unsigned)g.W);
+    t /= (unsigned)g.W;
+    const int h = (int)(t % (unsigned)g.H);
+    const int n = (int)(t / (unsigned)g.H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // outputs p with p*s - pad <= h <= p*s - pad + k - 1
     const int hp = h + g.pad, wp = w + g.pad;
