@@ -439,7 +439,9 @@ dtg::BnEpi bn_bwd_epi(Tensor& part, const Tensor& x, const Tensor& mean, const T
 std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::optional<Tensor> x,
                                    c10::optional<Tensor> mean, c10::optional<Tensor> invstd,
                                    c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
-                                   c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled) {
+                                   c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled,
+                                   c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
+                                   c10::optional<Tensor> invstd2, c10::optional<Tensor> part2) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
@@ -473,6 +475,24 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
       TORCH_CHECK(mask.has_value() && mask->defined(), "mode 3 needs the mask tensor");
       CHECK_IN(*mask);
       bn.mode = 3;
+      if (x2.has_value() && x2->defined()) {  // second BN on the same gradient (projection shortcut)
+        TORCH_CHECK(mean2 && invstd2 && part2, "x2 needs mean2, invstd2 and part2");
+        CHECK_IN(*x2);
+        CHECK_DT(*x2, at::kBFloat16);
+        TORCH_CHECK(x2->numel() == (long long)M * N, "x2 shape mismatch");
+        for (const Tensor* t : {&*mean2, &*invstd2}) {
+          CHECK_IN(*t);
+          CHECK_DT(*t, at::kFloat);
+          TORCH_CHECK(t->numel() == N, "per-channel tensor size mismatch");
+        }
+        CHECK_IN(*part2);
+        CHECK_DT(*part2, at::kFloat);
+        TORCH_CHECK(part2->numel() == (long long)dtg::kBnStatSlots * 2 * N, "part2 size mismatch");
+        bn.x2 = cbfp(*x2);
+        bn.mean2 = mean2->data_ptr<float>();
+        bn.invstd2 = invstd2->data_ptr<float>();
+        bn.part2 = part2->data_ptr<float>();
+      }
       if (mask->scalar_type() == at::kByte) {  // packed bits [M, N/8]
         TORCH_CHECK(mask->numel() == (long long)M * (N / 8), "mask bits shape mismatch");
         bn.maskbits = mask->data_ptr<uint8_t>();
@@ -613,6 +633,40 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> bn_fwd2_part(Tensor x, Tensor
   return {y, m1, i1, m2, i2};
 }
 
+// dx, dx2 of two BNs fed by the same masked gradient dp (BN3 + projection BN), parameter gradients
+// accumulated into the given fp32 accumulators
+std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor gamma, Tensor smean, Tensor sinv,
+                                        Tensor dgamma, Tensor dbeta, Tensor x2, Tensor part2, Tensor gamma2,
+                                        Tensor smean2, Tensor sinv2, Tensor dgamma2, Tensor dbeta2) {
+  for (const Tensor* t : {&dp, &x, &x2}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kBFloat16);
+  }
+  TORCH_CHECK(x.dim() == 2 && dp.numel() == x.numel() && x2.sizes() == x.sizes(), "dp/x/x2 must be [M, C]");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "C must be a multiple of 8");
+  for (const Tensor* t : {&part, &part2}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  }
+  for (const Tensor* t : {&gamma, &smean, &sinv, &dgamma, &dbeta, &gamma2, &smean2, &sinv2, &dgamma2, &dbeta2}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(x.device());
+  auto dx = at::empty_like(x), dx2 = at::empty_like(x);
+  auto ws = at::empty({6LL * C}, x.options().dtype(at::kFloat));
+  dtg::bn_bwd2_from_part(cbfp(dp), cbfp(x), cbfp(x2), part.data_ptr<float>(), part2.data_ptr<float>(),
+                         gamma.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
+                         gamma2.data_ptr<float>(), smean2.data_ptr<float>(), sinv2.data_ptr<float>(), bfp(dx),
+                         bfp(dx2), dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dgamma2.data_ptr<float>(),
+                         dbeta2.data_ptr<float>(), ws.data_ptr<float>(), M, C, 1, cur_stream());
+  return {dx, dx2};
+}
+
 std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp, Tensor x, Tensor part, Tensor gamma,
                                                                        Tensor smean, Tensor sinv, bool want_dres,
                                                                        c10::optional<Tensor> dgamma_acc,
@@ -695,7 +749,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
         pybind11::arg("beta") = pybind11::none(), pybind11::arg("mask") = pybind11::none(),
-        pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false);
+        pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false,
+        pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none(),
+        pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none());
+  m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
+        pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
+  m.def("bn_bwd2_part", &bn_bwd2_part);
   m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("pooled") = false);
   m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),

@@ -27,10 +27,17 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   static_assert(MODE >= 1 && MODE <= 3, "BN epilogue mode");
   constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
   static_assert(C::NTH % CPR == 0, "fixed column group per thread");
-  static_assert(2 * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
+  static_assert((MODE == 3 ? 3 : 2) * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
   const int tid = threadIdx.x, cg = tid % CPR, n0 = bn0 + cg * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8], is[8], sc[8], sf[8];
+  // mode 3 with a second BN on the same gradient (x2: the projection shortcut's BN input): sum(dp*xhat2)
+  float q2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mu2[8], is2[8];
+  const bool two = MODE == 3 && bn.x2 != nullptr;
+  if (two && n0 < N) {
+    load8_f32(bn.mean2 + n0, mu2);
+    load8_f32(bn.invstd2 + n0, is2);
+  }
   if constexpr (MODE >= 2) {
     if (n0 < N) {
       float g[8], b[8];
@@ -86,6 +93,12 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         s[k] += d;
         q[k] += d * ((xv[k] - mu[k]) * is[k]);
       }
+      if (two) {
+        float x2v[8];
+        load8_bf16(bn.x2 + off, x2v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q2[k] += v[k] * ((x2v[k] - mu2[k]) * is2[k]);
+      }
       store8_bf16((bf16_t*)e.C + off, v);
     }
   });
@@ -96,9 +109,11 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   for (int k = 0; k < 8; ++k) {
     red[r * C::BN + cg * 8 + k] = s[k];
     red[(RW + r) * C::BN + cg * 8 + k] = q[k];
+    if (two) red[(2 * RW + r) * C::BN + cg * 8 + k] = q2[k];
   }
   __syncthreads();
-  float* part = bn.part + (long long)(tile_id % kBnStatSlots) * 2 * N;
+  const long long slot = (long long)(tile_id % kBnStatSlots) * 2 * N;
+  float* part = bn.part + slot;
   for (int c = tid; c < C::BN; c += C::NTH) {
     if (bn0 + c < N) {
       float ts = 0.f, tq = 0.f;
@@ -109,6 +124,13 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       }
       atomicAdd(part + bn0 + c, ts);
       atomicAdd(part + N + bn0 + c, tq);
+      if (two) {  // the second BN's partials: (sum dp, sum dp*xhat2), same finalize layout
+        float tq2 = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < RW; ++j) tq2 += red[(2 * RW + j) * C::BN + c];
+        atomicAdd(bn.part2 + slot + bn0 + c, ts);
+        atomicAdd(bn.part2 + slot + N + bn0 + c, tq2);
+      }
     }
   }
 }

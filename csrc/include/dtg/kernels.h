@@ -44,6 +44,12 @@ struct BnEpi {
   const float* beta = nullptr;
   const bf16_t* mask = nullptr;      // mode 3: relu mask as the bf16 block output (> 0) ...
   const uint8_t* maskbits = nullptr; // ... or as packed bits [M][N/8] (bit k of byte n/8 = column n+k)
+  // mode 3, optional: a second BN fed by the same gradient (the projection shortcut's): its input x2
+  // and statistics; (sum dp, sum dp*xhat2) go to part2 (same layout as part)
+  const bf16_t* x2 = nullptr;
+  const float* mean2 = nullptr;
+  const float* invstd2 = nullptr;
+  float* part2 = nullptr;
 };
 
 // ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
@@ -59,6 +65,12 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
                        const float* gamma2, const float* beta2, float* rmean2, float* rvar2, float* smean2,
                        float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st,
                        uint8_t* bits = nullptr);
+// two BNs fed by the same (relu-masked) gradient dp -- BN3 and the projection BN of a ResNet block:
+// dx = a*dp + bx*x + c0 and dx2 = a2*dp + bx2*x2 + c02 in one pass over dp (ws: 6C floats)
+void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, const float* part, const float* part2,
+                       const float* gamma, const float* smean, const float* sinv, const float* gamma2,
+                       const float* smean2, const float* sinv2, bf16_t* dx, bf16_t* dx2, float* dgamma, float* dbeta,
+                       float* dgamma2, float* dbeta2, float* ws, long long M, int C, int accum, hipStream_t st);
 // finish a backward BN from mode-2 partials: dx = a*dp + bx*x + c0 (ws: 3C floats), dres = dp if given
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,

@@ -528,6 +528,59 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
   DTG_TPR_SWITCH(g.tpr, bn_apply2_kernel<T><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa, bits));
 }
 
+// ---- bwd, projection blocks: dx = a*dp + bx*x + c0 and dx2 = a2*dp + bx2*x2 + c02, one read of dp -----
+template <int TPR>
+__global__ void __launch_bounds__(kBlk) bn_bwd_dx2_kernel(const bf16_t* __restrict__ dp, const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ x2,
+                                                          const float* __restrict__ coef,
+                                                          const float* __restrict__ coef2, bf16_t* __restrict__ dx,
+                                                          bf16_t* __restrict__ dx2, long long M, int C, long long rpc) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  if (c0 >= C) return;
+  float a[8], bx[8], cc[8], a2[8], bx2[8], cc2[8];
+  load8_f32(coef + c0, a);
+  load8_f32(coef + C + c0, bx);
+  load8_f32(coef + 2 * C + c0, cc);
+  load8_f32(coef2 + c0, a2);
+  load8_f32(coef2 + C + c0, bx2);
+  load8_f32(coef2 + 2 * C + c0, cc2);
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  for (long long m = m0 + ty; m < m1; m += RPP) {
+    const long long o = m * C + c0;
+    float g[8], xv[8], x2v[8], o1[8], o2[8];
+    load8_bf16(dp + o, g);
+    load8_bf16(x + o, xv);
+    load8_bf16(x2 + o, x2v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o1[k] = fmaf(a[k], g[k], fmaf(bx[k], xv[k], cc[k]));
+      o2[k] = fmaf(a2[k], g[k], fmaf(bx2[k], x2v[k], cc2[k]));
+    }
+    store8_bf16(dx + o, o1);
+    store8_bf16(dx2 + o, o2);
+  }
+}
+
+void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, const float* part, const float* part2,
+                       const float* gamma, const float* smean, const float* sinv, const float* gamma2,
+                       const float* smean2, const float* sinv2, bf16_t* dx, bf16_t* dx2, float* dgamma, float* dbeta,
+                       float* dgamma2, float* dbeta2, float* ws, long long M, int C, int accum, hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+                                                    nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
+                                                    0.f, ws, dgamma, dbeta, 1);
+  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, accum ? 2 : 1, gamma2, nullptr,
+                                                    nullptr, nullptr, const_cast<float*>(smean2),
+                                                    const_cast<float*>(sinv2), 0.f, 0.f, ws + 3LL * C, dgamma2,
+                                                    dbeta2, 1);
+  const long long rpa = elementwise_rpc(g, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
+  DTG_TPR_SWITCH(g.tpr, bn_bwd_dx2_kernel<T><<<ga, kBlk, 0, st>>>(dp, x, x2, ws, ws + 3LL * C, dx, dx2, M, C, rpa));
+}
+
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,

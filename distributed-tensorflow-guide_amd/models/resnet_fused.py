@@ -59,13 +59,16 @@ _LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction 
 
 
 class _Bn3Link:
-    """Block i's BN3 tensors, filled with the mode-3 partials by block i+1's backward."""
-    __slots__ = ("y3", "m3", "i3", "gamma", "beta", "bits", "part", "dp")
+    """Block i's BN3 tensors, filled with the mode-3 partials by block i+1's backward.  For a projection
+    block also its shortcut BN's input and statistics (yd, md, idd): the same masked gradient feeds
+    that BN, so block i+1's epilogue reduces its statistics too (part2)."""
+    __slots__ = ("y3", "m3", "i3", "gamma", "beta", "bits", "yd", "md", "idd", "part", "part2", "dp")
 
-    def __init__(self, y3, m3, i3, gamma, beta, bits):
+    def __init__(self, y3, m3, i3, gamma, beta, bits, yd=None, md=None, idd=None):
         self.y3, self.m3, self.i3, self.gamma, self.beta = y3, m3, i3, gamma, beta
         self.bits = bits  # packed (out > 0): the relu mask, 1/16 of the bytes of re-reading out
-        self.part = self.dp = None
+        self.yd, self.md, self.idd = yd, md, idd
+        self.part = self.part2 = self.dp = None
 
 
 def _gacc(p):
@@ -139,7 +142,7 @@ class _BottleneckFn(torch.autograd.Function):
                                          b3.eps, True)
         ctx.blk = blk
         ctx.link_in = link_in if (_FUSE and _LINK) else None
-        ctx.link_out = _Bn3Link(y3, m3, i3, b3.weight, b3.bias, bits) if (_FUSE and _LINK) else None
+        ctx.link_out = _Bn3Link(y3, m3, i3, b3.weight, b3.bias, bits, yd, md, idd) if (_FUSE and _LINK) else None
         holder.append(ctx.link_out)
         ctx.geom = (n, c, h, w, st, width, cout, p_, q_)
         ctx.save_for_backward(x2, y1, a1, m1, i1, y2, a2, m2, i2, y3, out, m3, i3,
@@ -163,18 +166,26 @@ class _BottleneckFn(torch.autograd.Function):
         do = _rows(dout)
         # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
         lk = ctx.link_out
+        dyd = None
         if (lk is not None and lk.part is not None and do.data_ptr() == lk.dp.data_ptr()
                 and do.shape == lk.dp.shape):
             # block i+1 already masked dL/d out (do is dp) and reduced this BN's statistics
-            dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
+            if lk.part2 is not None:  # ... and the shortcut BN's: both dx in one pass over dp
+                bd = blk.down.bn
+                dy3, dyd = L.bn_bwd2_part(do, y3, lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)],
+                                          sv[13], lk.part2, bd.weight, sv[14], sv[15], g[id(bd.weight)],
+                                          g[id(bd.bias)])
+            else:
+                dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
             dres = do  # our own buffer (pointer-checked above): dx accumulates into it in place
         else:
-            if lk is not None and lk.part is not None:
-                lk.part.zero_()  # pooled slots must go back zeroed (see bn_part in csrc/bindings/ops.cc)
+            for pt in ((lk.part, lk.part2) if lk is not None else ()):
+                if pt is not None:
+                    pt.zero_()  # pooled slots must go back zeroed (see bn_part in csrc/bindings/ops.cc)
             dy3, dres, _, _ = L.bn_bwd(do, out, y3, b3.weight, m3, i3, True, True, g[id(b3.weight)],
                                        g[id(b3.bias)])
         if lk is not None:
-            lk.part = lk.dp = None
+            lk.part = lk.part2 = lk.dp = None
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
         if _FUSE:
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
@@ -207,8 +218,9 @@ class _BottleneckFn(torch.autograd.Function):
         if blk.down is not None:
             yd, md, idd = sv[13:16]
             bd, wd = blk.down.bn, blk.down.conv.weight
-            dyd, _, _, _ = L.bn_bwd(dres, None, yd, bd.weight, md, idd, False, False, g[id(bd.weight)],
-                                    g[id(bd.bias)])
+            if dyd is None:
+                dyd, _, _, _ = L.bn_bwd(dres, None, yd, bd.weight, md, idd, False, False, g[id(bd.weight)],
+                                        g[id(bd.bias)])
             if st == 1:
                 dx2 = gemm(dyd, True, _mat(wd), False)
                 gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
@@ -227,9 +239,13 @@ class _BottleneckFn(torch.autograd.Function):
             dx2 = dres
         if not dx_done:
             if lk_in is not None:  # mode 3: finish the previous block's BN3 reduction in this epilogue
+                part2 = None
+                if lk_in.yd is not None:  # the previous block is a projection block: its shortcut BN too
+                    part2 = L.bn_part_alloc(dy1, c, pooled=True)
                 _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                    mask=lk_in.bits, out=dx2, pooled=True)
-                lk_in.part, lk_in.dp = part, dx2
+                                    mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
+                                    invstd2=lk_in.idd, part2=part2)
+                lk_in.part, lk_in.part2, lk_in.dp = part, part2, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
         gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
