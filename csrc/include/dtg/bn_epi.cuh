@@ -24,19 +24,21 @@ namespace gemm {
 template <class C, int MODE, class ROWMAP>
 __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                             const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
-  static_assert(MODE >= 1 && MODE <= 3, "BN epilogue mode");
+  static_assert(MODE >= 1 && MODE <= 4, "BN epilogue mode");  // 4 = mode 3 + a second BN (x2)
   constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
   static_assert(C::NTH % CPR == 0, "fixed column group per thread");
-  static_assert((MODE == 3 ? 3 : 2) * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
+  static_assert((MODE == 4 ? 3 : 2) * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
   const int tid = threadIdx.x, cg = tid % CPR, n0 = bn0 + cg * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[8], is[8], sc[8], sf[8];
   // mode 3 with a second BN on the same gradient (x2: the projection shortcut's BN input): sum(dp*xhat2)
   float q2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mu2[8], is2[8];
-  const bool two = MODE == 3 && bn.x2 != nullptr;
-  if (two && n0 < N) {
-    load8_f32(bn.mean2 + n0, mu2);
-    load8_f32(bn.invstd2 + n0, is2);
+  constexpr bool two = MODE == 4;  // a separate instantiation: mode 3 keeps its register budget
+  if constexpr (two) {
+    if (n0 < N) {
+      load8_f32(bn.mean2 + n0, mu2);
+      load8_f32(bn.invstd2 + n0, is2);
+    }
   }
   if constexpr (MODE >= 2) {
     if (n0 < N) {
@@ -93,7 +95,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         s[k] += d;
         q[k] += d * ((xv[k] - mu[k]) * is[k]);
       }
-      if (two) {
+      if constexpr (two) {
         float x2v[8];
         load8_bf16(bn.x2 + off, x2v);
 #pragma unroll
@@ -109,7 +111,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   for (int k = 0; k < 8; ++k) {
     red[r * C::BN + cg * 8 + k] = s[k];
     red[(RW + r) * C::BN + cg * 8 + k] = q[k];
-    if (two) red[(2 * RW + r) * C::BN + cg * 8 + k] = q2[k];
+    if constexpr (two) red[(2 * RW + r) * C::BN + cg * 8 + k] = q2[k];
   }
   __syncthreads();
   const long long slot = (long long)(tile_id % kBnStatSlots) * 2 * N;
@@ -124,7 +126,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       }
       atomicAdd(part + bn0 + c, ts);
       atomicAdd(part + N + bn0 + c, tq);
-      if (two) {  // the second BN's partials: (sum dp, sum dp*xhat2), same finalize layout
+      if constexpr (two) {  // the second BN's partials: (sum dp, sum dp*xhat2), same finalize layout
         float tq2 = 0.f;
 #pragma unroll 8
         for (int j = 0; j < RW; ++j) tq2 += red[(2 * RW + j) * C::BN + c];

@@ -279,6 +279,7 @@ void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
   Epi e{C, ldc, 1, 1.f, bn.mode == 3 ? beta : 0.f, nullptr, 0};
   if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (bn.x2) gemm_bn_dispatch<4>(A, lda, B, ldb, M, N, K, e, bn, st);
   else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
