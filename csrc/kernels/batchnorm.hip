@@ -109,14 +109,16 @@ __global__ void __launch_bounds__(kBlk) bn_stats_kernel(const bf16_t* __restrict
 //                save_mean/save_invstd, running stats update.
 // mode 1 (bwd):  a = gamma*invstd; dgamma = sum(dp*xhat), dbeta = sum(dp);
 //                dx = a*dp + bx*x + c0   with bx = -a*invstd*dgamma/M, c0 = -a*dbeta/M - bx*mean
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ part, int nchunk, long long M,
+// G chunk groups per channel (16 = 1024 threads; 4 = 256 threads measured slower for the 32 epilogue
+// slots too: the kernel is latency-, not occupancy-bound)
+template <int G = 16>
+__global__ void __launch_bounds__(64 * G) bn_finalize_kernel(const float* __restrict__ part, int nchunk, long long M,
                                                            int C, int mode, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* __restrict__ rmean,
                                                            float* __restrict__ rvar, float* __restrict__ smean,
                                                            float* __restrict__ sinv, float momentum, float eps,
                                                            float* __restrict__ coef, float* __restrict__ dgamma,
                                                            float* __restrict__ dbeta, int zero_after = 0) {
-  constexpr int G = 16;  // chunk groups per channel
   __shared__ double sh[2][G][64];
   const int cl = threadIdx.x % 64, r = threadIdx.x / 64;
   const int c = blockIdx.x * 64 + cl;
@@ -439,7 +441,7 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
   float* coef = ws + (long long)g.nchunk * 2 * C;
   dim3 grid(g.nchunk, g.gy);
   DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
                                                     momentum, eps, coef, nullptr, nullptr);
   bn_apply_launch(g, x, res, y, coef, M, C, relu, st);
 }
@@ -449,7 +451,7 @@ void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float
                       float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
                       int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
                                                     sinv, momentum, eps, ws, nullptr, nullptr, 1);
   bn_apply_launch(g, x, res, y, ws, M, C, relu, st, bits);
 }
@@ -496,7 +498,7 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
     if (relu) bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
     else bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
   });
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr, nullptr,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr, nullptr,
                                                     const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
                                                     coef, dgamma, dbeta);
   const long long rpa = elementwise_rpc(g, M);
@@ -519,9 +521,9 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
                        float* sinv2, float* ws, long long M, int C, float momentum, float eps, hipStream_t st,
                        uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
                                                     sinv, momentum, eps, ws, nullptr, nullptr, 1);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, 0, gamma2, beta2, rmean2, rvar2,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, 0, gamma2, beta2, rmean2, rvar2,
                                                     smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
@@ -569,10 +571,10 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
                        const float* smean2, const float* sinv2, bf16_t* dx, bf16_t* dx2, float* dgamma, float* dbeta,
                        float* dgamma2, float* dbeta2, float* ws, long long M, int C, int accum, hipStream_t st) {
   const BnGeom g = bn_geom(M, C);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
                                                     0.f, ws, dgamma, dbeta, 1);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, accum ? 2 : 1, gamma2, nullptr,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, accum ? 2 : 1, gamma2, nullptr,
                                                     nullptr, nullptr, const_cast<float*>(smean2),
                                                     const_cast<float*>(sinv2), 0.f, 0.f, ws + 3LL * C, dgamma2,
                                                     dbeta2, 1);
@@ -586,7 +588,7 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
                       int C, int accum, hipStream_t st) {
   const BnGeom g = bn_geom(M, C);
-  bn_finalize_kernel<<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
                                                     0.f, ws, dgamma, dbeta, 1);
   const long long rpa = elementwise_rpc(g, M);
