@@ -46,9 +46,14 @@ constexpr int NT = 256;
 
 // BK_ = K depth of one ring stage: 64 (128-B LDS rows) or 32 (64-B rows: half the LDS per stage, so a
 // deep ring still leaves room for several workgroups per CU).
-template <int BM_, int BN_, int STAGES_ = 2, int NW_ = 4, int BK_ = 64>
+// RP_ (single-stage only): register pipelining -- each K-step's operand fragments are read from LDS into
+// registers up front, so the next step's LDS-DMA can be issued before this step's MFMAs (one LDS
+// buffer, DMA latency overlapped with the MFMAs instead of exposed).
+template <int BM_, int BN_, int STAGES_ = 2, int NW_ = 4, int BK_ = 64, bool RP_ = false>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, STAGES = STAGES_, NW = NW_, NTH = NW_ * 64, BK = BK_;
+  static constexpr bool RP = RP_;
+  static_assert(!RP_ || STAGES_ == 1, "register pipelining is a single-stage schedule");
   static constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == NW, "one 64x64 sub-tile per wave");
   static_assert(STAGES >= 1 && STAGES <= 5, "ring depth");
@@ -233,7 +238,45 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
   constexpr int BK = C::BK;
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk <= 0) return;
-  if constexpr (C::STAGES == 1) {
+  if constexpr (C::STAGES == 1 && C::RP) {
+    constexpr int KS = BK / 32;
+    v8bf a[KS][4], b[KS][4];
+    auto read_frags = [&]() {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[ks][i] = frag<AKC, C::BM, BK>(smem, wm * 64 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[ks][j] = frag<BKC, C::BN, BK>(smem + C::A_BYTES, wn * 64 + j * 16, ks, lane);
+      }
+    };
+    sta(smem, kbeg);
+    stb(smem + C::A_BYTES, kbeg);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_frags();
+    __syncthreads();  // every wave holds its fragments: the LDS buffer is free for the next DMA
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        sta(smem, kbeg + (kt + 1) * BK);
+        stb(smem + C::A_BYTES, kbeg + (kt + 1) * BK);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
+      if (more) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        read_frags();
+        __syncthreads();
+      }
+    }
+  } else if constexpr (C::STAGES == 1) {
     for (int kt = 0; kt < nk; ++kt) {
       sta(smem, kbeg + kt * BK);
       stb(smem + C::A_BYTES, kbeg + kt * BK);

@@ -438,15 +438,23 @@ static int g_conv_stages[3] = {0, 0, 0};
 static int conv_stages(int which, long long M = 0, int N = 0, int Kred = 0) {
   if (g_conv_stages[which] == 0) {
     const char* f = getenv("DTG_CONV_STAGES");
-    g_conv_stages[which] = f ? (atoi(f) == 1 ? 1 : 2) : -1;
+    g_conv_stages[which] = f ? (atoi(f) >= 1 && atoi(f) <= 3 ? atoi(f) : 2) : -1;
   }
   if (g_conv_stages[which] > 0) return g_conv_stages[which];
   if (which == 2) return 1;
   const long long tiles = ((M + 127) / 128) * ((N + 127) / 128);
   return (tiles < 512 && Kred >= 2048) ? 2 : 1;
 }
+// schedule code: 1 = single LDS stage, 2 = two-stage ring, 3 = single stage, register-pipelined (Cfg RP)
 void conv_set_stages(int which, int stages) {  // 0 restores the measured default
-  if (which >= 0 && which < 3) g_conv_stages[which] = stages == 1 ? 1 : (stages == 2 ? 2 : -1);
+  if (which >= 0 && which < 3) g_conv_stages[which] = stages >= 1 && stages <= 3 ? stages : -1;
+}
+
+template <int BM, int BN, class F>
+static void run_sched(int sched, F&& run) {
+  if (sched == 1) run(Cfg<BM, BN, 1>());
+  else if (sched == 2) run(Cfg<BM, BN, 2>());
+  else run(Cfg<BM, BN, 1, 4, 64, true>());
 }
 
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
@@ -467,9 +475,9 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
     if (bn.mode == 1) conv_fwd_kernel<CF, 1><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
     else conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
   };
-  const bool s1 = conv_stages(0, M, K, R * S * C) == 1;
-  if (conv_skinny(K)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
-  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  const int sc = conv_stages(0, M, K, R * S * C);
+  if (conv_skinny(K)) run_sched<256, 64>(sc, run);
+  else run_sched<128, 128>(sc, run);
 }
 
 // 8-channel input (the stem, zero padded 3 -> 8); w is [K][Kp], Kp = ceil64(R*S*8), (r, s, c) order
@@ -486,6 +494,12 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
   };
   if (conv_skinny(K)) run(Cfg<256, 64, 1>());
   else run(Cfg<128, 128, 1>());
+}
+
+// 3x3 data gradients on 128x128 tiles: the register-pipelined schedule is 5-13 % faster on every
+// ResNet-50 layer with C >= 128 (profiles/r01_tiles/lr_conv_rp.txt); everything else lost with it
+static int dgrad_sched(int sc, const ConvGeom& G) {
+  return (g_conv_stages[1] <= 0 && G.R * G.S > 1) ? 3 : sc;
 }
 
 static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
@@ -532,14 +546,14 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
     return a.nr * a.ns > b.nr * b.ns;
   });
   const dim3 grid(max_tiles, nc);
-  const bool s1 = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s)) == 1;
+  const int sc = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s));
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     if (bn.mode == 2) conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
     else conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
   };
-  if (skinny) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
-  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  if (skinny) run_sched<256, 64>(sc, run);
+  else run_sched<128, 128>(dgrad_sched(sc, G), run);
   return 1;
 }
 
@@ -561,14 +575,14 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
     if (bn.mode == 2) conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
     else conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
   };
-  const bool s1 = conv_stages(1, M, C, R * S * K) == 1;
-  if (wT && s1) {
+  const int sc = conv_stages(1, M, C, R * S * K);
+  if (wT && sc == 1) {
     if (conv_skinny(C)) run_t(Cfg<256, 64, 1>());
     else run_t(Cfg<128, 128, 1>());
     return 1;
   }
-  if (conv_skinny(C)) s1 ? run(Cfg<256, 64, 1>()) : run(Cfg<256, 64, 2>());
-  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  if (conv_skinny(C)) run_sched<256, 64>(sc, run);
+  else run_sched<128, 128>(dgrad_sched(sc, G), run);
   return 1;
 }
 
@@ -599,9 +613,9 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
     dim3 grid(tm * tn, split);
     conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
   };
-  const bool s1 = conv_stages(2) == 1;
-  if (K <= 64) s1 ? run(Cfg<64, 256, 1>()) : run(Cfg<64, 256, 2>());  // 64 output channels: one 64-row tile
-  else s1 ? run(Cfg<128, 128, 1>()) : run(Cfg<128, 128, 2>());
+  const int sc = conv_stages(2);
+  if (K <= 64) run_sched<64, 256>(sc, run);  // 64 output channels: one 64-row tile
+  else run_sched<128, 128>(sc, run);
   gemm_splitk_reduce(ws, split, K, No, e, st);
 }
 

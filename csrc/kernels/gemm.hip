@@ -167,6 +167,12 @@ static void launch_big(int a_kc, int b_kc, const bf16_t* A, long long lda, const
 bool gemm_launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb,
                         int M, int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
                         const GemmBatch& bt);
+// DTG_GEMM_RP=0 turns off the register-pipelined single-stage tile (A/B switch)
+static bool gemm_rp() {
+  static const bool on = !(getenv("DTG_GEMM_RP") && getenv("DTG_GEMM_RP")[0] == '0');
+  return on;
+}
+
 static int g_forced_cfg = -1;
 static int forced_cfg() {
   if (g_forced_cfg < 0) {
@@ -213,8 +219,10 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   if (split_k > 1 || !a_kc) {
     // weight gradients (MN-contiguous A, split-K over the token/pixel dimension): the single-stage
     // 128x128 ring beat every other tile and the 2-stage ring on all of them, BERT's 768x3072x8192
-    // by 1.4x (profiles/r01_tiles/sweep_wgrad.json)
-    launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    // by 1.4x (profiles/r01_tiles/sweep_wgrad.json); its register-pipelined variant (next K-step's DMA
+    // issued under this step's MFMAs) is another 5-8 % on all wgrad shapes but one (sweep_rp.json)
+    if (gemm_rp()) launch_exact<Cfg<128, 128, 1, 4, 64, true>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    else launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
     return;
   }
   if (short_m(M, N)) {  // 64-row outputs: no half-empty 128-row tiles
@@ -230,7 +238,9 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
   // (< 512 tiles) and K long enough (>= 2048) that in-block prefetch pays (profiles/r01_tiles).
   const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * split_k * bt.count;
-  if (tiles128 < 512 && kps >= 2048) {
+  if (kps >= 2048 && gemm_rp()) {  // long K: the register-pipelined single stage beats both rings (sweep_rp.json)
+    launch_exact<Cfg<128, 128, 1, 4, 64, true>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+  } else if (tiles128 < 512 && kps >= 2048) {
     launch_exact<Cfg<128, 128, 2>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else if (skinny(N)) {
     launch_exact<Cfg<256, 64, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
@@ -266,8 +276,9 @@ template <int MODE>
 static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                              const Epi& e, const BnEpi& bn, hipStream_t st) {
   // same tile choice as gemm_bf16's heuristic
-  const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
-  if (tiles128 < 512 && K >= 2048) launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  if (K >= 2048 && gemm_rp()) launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if ((long long)((M + 127) / 128) * ((N + 127) / 128) < 512 && K >= 2048)
+    launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (skinny(N)) launch_bn_cfg<Cfg<256, 64, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (N >= 256 && M >= 64 && K <= 256) launch_bn_cfg<Cfg<64, 256, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);

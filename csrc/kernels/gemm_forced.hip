@@ -36,6 +36,9 @@ bool gemm_launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long 
     DTG_CFG_CASE(22, Cfg<256, 64, 2, 4, 32>)
     DTG_CFG_CASE(23, Cfg<128, 128, 5, 4, 32>)
     DTG_CFG_CASE(24, Cfg<64, 256, 4, 4, 32>)
+    DTG_CFG_CASE(25, Cfg<128, 128, 1, 4, 64, true>)
+    DTG_CFG_CASE(26, Cfg<64, 256, 1, 4, 64, true>)
+    DTG_CFG_CASE(27, Cfg<256, 64, 1, 4, 64, true>)
     default: return false;
   }
 #undef DTG_CFG_CASE

@@ -23,7 +23,8 @@ NAMES = {0: "heur", 1: "128x128s1", 2: "128x128s2", 3: "128x128s3", 4: "128x128s
          7: "256x64s4", 8: "256x128s3w8", 9: "256x128s2w8", 10: "128x256s2w8", 11: "128x256s3w8", 12: "64x256s2",
          13: "64x256s3", 14: "256x64s1", 15: "64x256s1", 16: "128x128s2k32",
          17: "128x128s3k32", 18: "128x128s4k32", 19: "64x256s3k32", 20: "256x64s3k32", 21: "64x256s2k32",
-         22: "256x64s2k32", 23: "128x128s5k32", 24: "64x256s4k32", 99: "8phase"}
+         22: "256x64s2k32", 23: "128x128s5k32", 24: "64x256s4k32", 25: "128x128s1rp", 26: "64x256s1rp", 27: "256x64s1rp",
+         99: "8phase"}
 
 # (M, N, K, a_kc, b_kc, beta): the memory-bound and mid-size GEMMs of a ResNet-50 batch-256 step
 SHAPES = [
@@ -77,7 +78,7 @@ def main():
         fl = 2.0 * M * N * K
         rows = []
         for c in cfgs:
-            if c in (5, 6, 7, 14, 20, 22) and N > 64 and N % 64:
+            if c in (5, 6, 7, 14, 20, 22, 27) and N > 64 and N % 64:
                 continue
             for split in splits:
                 L.gemm_force_cfg(c)
