@@ -531,9 +531,16 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
 }
 
 // dp = dgrad(dy, w) * relu'(bn(x)) with backward BN partials; x is the BN input [N,H,W,C]
+uint8_t* bits_ptr(const c10::optional<Tensor>& bits, long long M, int C) {
+  if (!bits.has_value() || !bits->defined()) return nullptr;
+  CHECK_IN(*bits);
+  TORCH_CHECK(bits->scalar_type() == at::kByte && bits->numel() == M * (C / 8), "bits must be uint8 [M, C/8]");
+  return bits->data_ptr<uint8_t>();
+}
+
 std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad,
                                          Tensor x, Tensor mean, Tensor invstd, Tensor gamma, Tensor beta,
-                                         bool pooled) {
+                                         bool pooled, c10::optional<Tensor> bits) {
   check_nhwc(dy, "dy");
   check_nhwc(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -545,19 +552,16 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t
   auto dx = at::empty({N, H, W, C}, dy.options());
   auto part = bn_part(dy, C, pooled);
   dtg::BnEpi bn = bn_bwd_epi(part, x, mean, invstd, gamma, beta, (long long)N * H * W, C);
+  if (uint8_t* mb = bits_ptr(bits, (long long)N * H * W, C)) {  // the forward's packed relu mask: mode 3, beta 0
+    bn.mode = 3;
+    bn.maskbits = mb;
+  }
   // stride 1: the kernel reads the weight transposed to [C][(r,s,k)] (K-contiguous; ~1 MB, one small copy)
   Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();
   TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn,
                               wT.defined() ? cbfp(wT) : nullptr),
               "conv_dgrad_bn: geometry leaves rows unwritten (use conv_dgrad + bn_bwd)");
   return {dx, part};
-}
-
-uint8_t* bits_ptr(const c10::optional<Tensor>& bits, long long M, int C) {
-  if (!bits.has_value() || !bits->defined()) return nullptr;
-  CHECK_IN(*bits);
-  TORCH_CHECK(bits->scalar_type() == at::kByte && bits->numel() == M * (C / 8), "bits must be uint8 [M, C/8]");
-  return bits->data_ptr<uint8_t>();
 }
 
 // bits (optional uint8 [M, C/8]) receives the packed (out > 0) relu mask
@@ -759,7 +763,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("pad"), pybind11::arg("pooled") = false);
   m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),
         pybind11::arg("W"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("x"), pybind11::arg("mean"),
-        pybind11::arg("invstd"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("pooled") = false);
+        pybind11::arg("invstd"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("pooled") = false,
+        pybind11::arg("bits") = pybind11::none());
   m.def("bn_fwd2_part", &bn_fwd2_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("gamma"),
         pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("r"), pybind11::arg("part2"),
         pybind11::arg("gamma2"), pybind11::arg("beta2"), pybind11::arg("rmean2"), pybind11::arg("rvar2"),

@@ -29,27 +29,25 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   static_assert(C::NTH % CPR == 0, "fixed column group per thread");
   static_assert((MODE == 4 ? 3 : 2) * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
   const int tid = threadIdx.x, cg = tid % CPR, n0 = bn0 + cg * 8;
+  // Backward modes accumulate the raw moment sum(d * x) and convert it once per column after the
+  // block reduction: sum(d * xhat) = invstd * (sum(d * x) - mean * sum(d)).  Keeping mean/invstd out of
+  // the row loop saves 16 VGPRs (32 in mode 4), which is what puts the 128x128 backward epilogues
+  // under the 128-VGPR line of 4 workgroups per CU.
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float mu[8], is[8], sc[8], sf[8];
-  // mode 3 with a second BN on the same gradient (x2: the projection shortcut's BN input): sum(dp*xhat2)
-  float q2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mu2[8], is2[8];
+  float sc[8], sf[8];
+  // mode 3 with a second BN on the same gradient (x2: the projection shortcut's BN input): sum(dp*x2)
+  float q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   constexpr bool two = MODE == 4;  // a separate instantiation: mode 3 keeps its register budget
-  if constexpr (two) {
+  if constexpr (MODE == 2) {  // the relu mask is recomputed from x: gamma*xhat + beta > 0
     if (n0 < N) {
-      load8_f32(bn.mean2 + n0, mu2);
-      load8_f32(bn.invstd2 + n0, is2);
-    }
-  }
-  if constexpr (MODE >= 2) {
-    if (n0 < N) {
-      float g[8], b[8];
+      float mu[8], is[8], g[8], b[8];
       load8_f32(bn.mean + n0, mu);
       load8_f32(bn.invstd + n0, is);
       load8_f32(bn.gamma + n0, g);
       load8_f32(bn.beta + n0, b);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        sc[k] = g[k] * is[k];       // = bn_finalize's coef (scale)
+        sc[k] = g[k] * is[k];          // = bn_finalize's coef (scale)
         sf[k] = b[k] - mu[k] * sc[k];  // = bn_finalize's coef (shift)
       }
     }
@@ -73,7 +71,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
         v[k] = d;
         s[k] += d;
-        q[k] += d * ((xv[k] - mu[k]) * is[k]);
+        q[k] += d * xv[k];
       }
       store8_bf16((bf16_t*)e.C + off, v);
     } else {
@@ -93,13 +91,13 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
         v[k] = d;
         s[k] += d;
-        q[k] += d * ((xv[k] - mu[k]) * is[k]);
+        q[k] += d * xv[k];
       }
       if constexpr (two) {
         float x2v[8];
         load8_bf16(bn.x2 + off, x2v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) q2[k] += v[k] * ((x2v[k] - mu2[k]) * is2[k]);
+        for (int k = 0; k < 8; ++k) q2[k] += v[k] * x2v[k];
       }
       store8_bf16((bf16_t*)e.C + off, v);
     }
@@ -124,12 +122,14 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         ts += red[j * C::BN + c];
         tq += red[(RW + j) * C::BN + c];
       }
+      if constexpr (MODE >= 2) tq = bn.invstd[bn0 + c] * (tq - bn.mean[bn0 + c] * ts);  // raw -> centred
       atomicAdd(part + bn0 + c, ts);
       atomicAdd(part + N + bn0 + c, tq);
       if constexpr (two) {  // the second BN's partials: (sum dp, sum dp*xhat2), same finalize layout
         float tq2 = 0.f;
 #pragma unroll 8
         for (int j = 0; j < RW; ++j) tq2 += red[(2 * RW + j) * C::BN + c];
+        tq2 = bn.invstd2[bn0 + c] * (tq2 - bn.mean2[bn0 + c] * ts);
         atomicAdd(bn.part2 + slot + bn0 + c, ts);
         atomicAdd(bn.part2 + slot + N + bn0 + c, tq2);
       }

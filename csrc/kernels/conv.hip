@@ -550,6 +550,7 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     if (bn.mode == 2) conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
+    else if (bn.mode == 3) conv_dgrad_s_kernel<CF, 3><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
     else conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
   };
   if (skinny) run_sched<256, 64>(sc, run);
@@ -567,12 +568,14 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
     if (bn.mode == 2) conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
+    else if (bn.mode == 3) conv_dgrad_kernel<CF, 3><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
     else conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
   };
   auto run_t = [&](auto cf) {  // K-contiguous transposed weights
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
     if (bn.mode == 2) conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
+    else if (bn.mode == 3) conv_dgrad_kernel<CF, 3, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
     else conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
   };
   const int sc = conv_stages(1, M, C, R * S * K);

@@ -78,6 +78,15 @@ def _gacc(p):
     return torch.zeros_like(p, dtype=torch.float32 if p.dim() <= 1 else p.dtype), False
 
 
+# DTG_BN_BITS=0: the backward recomputes BN1/BN2's relu masks from y and the BN statistics (mode 2)
+# instead of reading the packed masks the forward apply wrote (mode 3, 1/16 of y's bytes)
+_BITS = os.environ.get("DTG_BN_BITS", "1") != "0"
+
+
+def _relu_bits(y):
+    return torch.empty(y.shape[0], y.shape[1] // 8, device=y.device, dtype=torch.uint8) if _BITS else None
+
+
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, blk, link_in, holder, *params):
@@ -92,12 +101,15 @@ class _BottleneckFn(torch.autograd.Function):
         w1, w2, w3 = blk.c1.conv.weight, blk.c2.conv.weight, blk.c3.conv.weight
         if _FUSE:
             y1, p1 = L.gemm_bn(x2, _mat(w1), 1, pooled=True)
+            bits1 = _relu_bits(y1)
             a1, m1, i1 = L.bn_fwd_part(y1, p1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var,
-                                       b1.momentum, b1.eps, True)
+                                       b1.momentum, b1.eps, True, bits=bits1)
             y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1, pooled=True)
             y2 = y2.view(-1, width)
+            bits2 = _relu_bits(y2)
             a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
-                                       b2.momentum, b2.eps, True)
+                                       b2.momentum, b2.eps, True, bits=bits2)
+            ctx.bits12 = (bits1, bits2)
             y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
         else:
             y1 = gemm(x2, True, _mat(w1), True)
@@ -187,7 +199,11 @@ class _BottleneckFn(torch.autograd.Function):
         if lk is not None:
             lk.part = lk.part2 = lk.dp = None
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
-        if _FUSE:
+        bits1, bits2 = ctx.bits12 if _FUSE else (None, None)
+        ctx.bits12 = None
+        if _FUSE and bits2 is not None:  # relu mask from the forward's bits: mode 3 with nothing to accumulate
+            dp2, q2 = L.gemm_bn(dy3, _mat(w3), 3, y2, m2, i2, b2.weight, b2.bias, mask=bits2, pooled=True)
+        elif _FUSE:
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
@@ -200,7 +216,7 @@ class _BottleneckFn(torch.autograd.Function):
         dy2_4 = dy2.view(n, p_, q_, width)
         if _FUSE:
             dp1, q1 = L.conv_dgrad_bn(dy2_4, _krsc(w2).contiguous(), h, w, st, 1, y1, m1, i1, b1.weight, b1.bias,
-                                       pooled=True)
+                                       pooled=True, bits=bits1)
             dp1 = dp1.view(-1, width)
         else:
             da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)

@@ -70,6 +70,17 @@ def test_gemm_bn_bwd_stats(M, N, K):
     s, q = _bn_stats(part, N)
     assert _rel(s, sr) < 1e-2
     assert _rel(q, qr) < 1e-2
+    # the same reduction with the relu mask read from packed bits (mode 3 without accumulation)
+    dp3, part3 = lib().gemm_bn(dy, w, 3, x, mean, inv, gamma, beta, mask=_pack_mask(x, mean, inv, gamma, beta))
+    assert _rel(dp3, dpr) < 1e-2
+    s3, q3 = _bn_stats(part3, N)
+    assert _rel(s3, sr) < 1e-2 and _rel(q3, qr) < 1e-2
+
+
+def _pack_mask(x, mean, inv, gamma, beta):
+    """uint8 [M, C/8]: bit k of byte j = relu mask of column 8j+k (gamma*xhat + beta > 0)."""
+    m = ((x.float() - mean) * inv * gamma + beta > 0).to(torch.int32).view(x.shape[0], -1, 8)
+    return (m << torch.arange(8, device=x.device, dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
 
 
 @pytest.mark.parametrize("C,K,H,R,st,pad", [(64, 64, 14, 3, 1, 1), (128, 128, 14, 3, 2, 1), (64, 256, 8, 1, 1, 0),
@@ -100,6 +111,13 @@ def test_conv_bn_fwd_and_dgrad_stats(C, K, H, R, st, pad):
     assert _rel(dp.view(-1, C), dpr) < 1e-2
     s, q = _bn_stats(part, C)
     assert _rel(s, sr) < 1e-2 and _rel(q, qr) < 1e-2
+    if st == 1 or R == 3:  # relu mask from packed bits (what the fused bottleneck passes)
+        bits = _pack_mask(xin.view(-1, C), mean, inv, gamma, beta)
+        dp3, part3 = L.conv_dgrad_bn(dy, w.permute(0, 2, 3, 1).contiguous(), H, H, st, pad, xin.view(-1, C), mean,
+                                     inv, gamma, beta, bits=bits)
+        assert _rel(dp3.view(-1, C), dpr) < 1e-2
+        s3, q3 = _bn_stats(part3, C)
+        assert _rel(s3, sr) < 1e-2 and _rel(q3, qr) < 1e-2
 
 
 @pytest.mark.parametrize("res", [False, True])
