@@ -496,10 +496,11 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
   else run(Cfg<128, 128, 1>());
 }
 
-// 3x3 data gradients on 128x128 tiles: the register-pipelined schedule is 5-13 % faster on every
-// ResNet-50 layer with C >= 128 (profiles/r01_tiles/lr_conv_rp.txt); everything else lost with it
+// 128x128 data gradients: where the default picks the 2-stage ring (short grid, long K: the 7x7 3x3
+// layers) the register-pipelined single stage is 10 % faster; elsewhere the plain single stage wins
+// now that the mode-3 epilogue fits 4 workgroups per CU (profiles/r01_rp/lr_dgrad_sched.txt)
 static int dgrad_sched(int sc, const ConvGeom& G) {
-  return (g_conv_stages[1] <= 0 && G.R * G.S > 1) ? 3 : sc;
+  return (g_conv_stages[1] <= 0 && G.R * G.S > 1 && sc == 2) ? 3 : sc;
 }
 
 static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
