@@ -290,7 +290,7 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
     auxp = aux->data_ptr();
   }
   c10::DeviceGuard dg(A.device());
-  int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K);
+  int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K, a_kc ? 1 : 0);
   Tensor ws;
   float* wsp = nullptr;
   if (sk > 1) {

@@ -99,7 +99,7 @@ struct GemmBatch {
 // force one GEMM tile configuration (sweeps; 0 = heuristic, 99 = 8-phase 256x256)
 void gemm_force_cfg(int cfg);
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
-int gemm_pick_split(int M, int N, int K);
+int gemm_pick_split(int M, int N, int K, int a_kc = 0);
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                int split_k, float* ws, hipStream_t st, const GemmBatch& batch = GemmBatch(), void* aux = nullptr,

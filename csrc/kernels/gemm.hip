@@ -94,9 +94,13 @@ static bool skinny(int N) { return N <= 64; }
 
 static bool short_m(int M, int N) { return M <= 64 && N >= 128; }
 
-int gemm_pick_split(int M, int N, int K) {
+int gemm_pick_split(int M, int N, int K, int a_kc) {
   const int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
+  // forward / data-gradient GEMMs (K-contiguous A) with >= 128 tiles: the fp32 partial round trip
+  // costs more than the idle CUs do (BERT 8192x768x3072: 47 us unsplit, 56 us split 2;
+  // profiles/r01_rp/sweep_bert.log)
+  if (a_kc && tiles >= 128) return 1;
   int s = 1;
   // aim for >= ~512 workgroups (2 per CU: the LDS ring admits 2) while keeping >= 1024 K
   // (16 K-steps) per split
@@ -173,6 +177,17 @@ static bool gemm_rp() {
   return on;
 }
 
+// Register pipelining pays when each workgroup has a long K loop and the problem is compute-heavy
+// enough that latency, not occupancy (3 instead of 4 workgroups per CU), limits it: long K (>= 2048),
+// or K >= 768 at >= 300 flop per operand byte (BERT's 8192-token GEMMs: 5-12 % faster; ResNet's
+// 50176x256x1024 at 204 flop/B is 8 % slower with it).
+static bool use_rp(int M, int N, int kps) {
+  if (!gemm_rp()) return false;
+  if (kps >= 2048) return true;
+  const double flop = 2.0 * M * N * kps, bytes = 2.0 * ((double)M * kps + (double)N * kps + (double)M * N);
+  return kps >= 768 && flop / bytes >= 300.0;
+}
+
 static int g_forced_cfg = -1;
 static int forced_cfg() {
   if (g_forced_cfg < 0) {
@@ -238,7 +253,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
   // (< 512 tiles) and K long enough (>= 2048) that in-block prefetch pays (profiles/r01_tiles).
   const long long tiles128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * split_k * bt.count;
-  if (kps >= 2048 && gemm_rp()) {  // long K: the register-pipelined single stage beats both rings (sweep_rp.json)
+  if (use_rp(M, N, kps)) {  // the register-pipelined single stage (sweep_rp.json, sweep_bert.log)
     launch_exact<Cfg<128, 128, 1, 4, 64, true>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
   } else if (tiles128 < 512 && kps >= 2048) {
     launch_exact<Cfg<128, 128, 2>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
@@ -276,7 +291,7 @@ template <int MODE>
 static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                              const Epi& e, const BnEpi& bn, hipStream_t st) {
   // same tile choice as gemm_bf16's heuristic
-  if (K >= 2048 && gemm_rp()) launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+  if (use_rp(M, N, K)) launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if ((long long)((M + 127) / 128) * ((N + 127) / 128) < 512 && K >= 2048)
     launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (skinny(N)) launch_bn_cfg<Cfg<256, 64, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);

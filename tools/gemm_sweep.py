@@ -41,6 +41,10 @@ SHAPES = [
     # BERT-base weight gradients (tokens = 64 x 128)
     (768, 3072, 8192, False, False, 1.0), (3072, 768, 8192, False, False, 1.0), (2304, 768, 8192, False, False, 1.0),
     (768, 768, 8192, False, False, 1.0),
+    # BERT-base batch 64 x 128 forward / data-gradient GEMMs (B = W as [out, in]: KC forward, MC dgrad)
+    (8192, 768, 3072, True, False, 0.0), (8192, 768, 2304, True, False, 0.0), (8192, 3072, 768, True, False, 0.0),
+    (8192, 768, 3072, True, True, 0.0), (8192, 3072, 768, True, True, 0.0), (8192, 2304, 768, True, True, 0.0),
+    (8192, 768, 768, True, True, 0.0),
 ]
 
 
