@@ -11,6 +11,7 @@
 // row of H = 768 is 96 chunks -> every load is a dwordx4 and reductions are wave shuffles.
 #include "dtg/common.h"
 #include "dtg/kernels.h"
+#include <stdlib.h>
 
 namespace dtg {
 
@@ -131,18 +132,51 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
   for (int j = 0; j < NCH; ++j)
 #pragma unroll
     for (int k = 0; k < 8; ++k) dg[j][k] = db[j][k] = dz[j][k] = 0.f;
-  for (int row = blockIdx.x * kRowsPerBlock + wv; row < T; row += gridDim.x * kRowsPerBlock) {
+  // One row ahead in registers: the next row's dy / s (and its statistics) are loaded before this
+  // row's reductions and stores, so each wave keeps two rows of HBM reads in flight (2 blocks per CU
+  // leave too few waves to hide the latency otherwise).
+  const int rstep = gridDim.x * kRowsPerBlock;
+  int row = blockIdx.x * kRowsPerBlock + wv;
+  uint4 pdy[NCH], ps[NCH];
+  float pmean = 0.f, prstd = 0.f;
+  auto prefetch = [&](int r) {
+    if (r >= T) return;
+    const long long b = (long long)r * H;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nc) {
+        pdy[j] = *reinterpret_cast<const uint4*>(dy + b + c * 8);
+        ps[j] = *reinterpret_cast<const uint4*>(s + b + c * 8);
+      }
+    }
+    pmean = mean_in[r];
+    prstd = rstd_in[r];
+  };
+  prefetch(row);
+  for (; row < T; row += rstep) {
     const long long base = (long long)row * H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    const float mean = pmean, rstd = prstd;
     float g[NCH][8], xh[NCH][8];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const uint4 u = pdy[j], w = ps[j];
+      g[j][0] = __uint_as_float(u.x << 16); g[j][1] = __uint_as_float(u.x & 0xffff0000u);
+      g[j][2] = __uint_as_float(u.y << 16); g[j][3] = __uint_as_float(u.y & 0xffff0000u);
+      g[j][4] = __uint_as_float(u.z << 16); g[j][5] = __uint_as_float(u.z & 0xffff0000u);
+      g[j][6] = __uint_as_float(u.w << 16); g[j][7] = __uint_as_float(u.w & 0xffff0000u);
+      xh[j][0] = __uint_as_float(w.x << 16); xh[j][1] = __uint_as_float(w.x & 0xffff0000u);
+      xh[j][2] = __uint_as_float(w.y << 16); xh[j][3] = __uint_as_float(w.y & 0xffff0000u);
+      xh[j][4] = __uint_as_float(w.z << 16); xh[j][5] = __uint_as_float(w.z & 0xffff0000u);
+      xh[j][6] = __uint_as_float(w.w << 16); xh[j][7] = __uint_as_float(w.w & 0xffff0000u);
+    }
+    prefetch(row + rstep);
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const int c = lane + 64 * j;
       if (c < nc) {
         float gm[8];
-        load8_bf16(dy + base + c * 8, g[j]);
-        load8_bf16(s + base + c * 8, xh[j]);
         load8_f32(gamma + c * 8, gm);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -476,9 +510,21 @@ void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float*
 #undef DTG_LNF
 }
 
+// Blocks of the LayerNorm backward (each folds its rows' dgamma/dbeta/dbias into one partial row of
+// the workspace).  DTG_LN_BWD_BLOCKS overrides the cap (A/B runs).
+static int ln_bwd_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* v = getenv("DTG_LN_BWD_BLOCKS");
+    cap = v ? atoi(v) : 512;
+    if (cap < 64) cap = 512;
+  }
+  return cap;
+}
+
 int ln_bwd_blocks(int T) {
-  const int b = (T + kRowsPerBlock - 1) / kRowsPerBlock;
-  return b < 512 ? (b < 1 ? 1 : b) : 512;
+  const int b = (T + kRowsPerBlock - 1) / kRowsPerBlock, cap = ln_bwd_cap();
+  return b < cap ? (b < 1 ? 1 : b) : cap;
 }
 
 void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* mean, const float* rstd,
