@@ -1,7 +1,5 @@
 #!/bin/bash
-# 1 PS + 2 workers on localhost (same launcher shape as the reference's run.sh files).
-cd "$(dirname "$0")"
-python AEASGD.py --job_name "ps" --task_index 0 "$@" &
-python AEASGD.py --job_name "worker" --task_index 0 "$@" &
-python AEASGD.py --job_name "worker" --task_index 1 "$@" &
-wait
+# AEASGD / AEAMSGD (elastic averaging): 1 PS + 2 workers on localhost.
+# Flags are forwarded to every task (e.g. --cluster '{"ps":[...],"worker":[...]}'); see ../launch_local.sh.
+here="$(cd "$(dirname "$0")" && pwd)"
+cd "$here" && exec bash ../launch_local.sh AEASGD.py 1 2 "$@"

@@ -1,9 +1,5 @@
 #!/bin/bash
-# DOWNPOUR-Easy: 1 PS + 2 asynchronous workers, local SGD window.
-# Extra flags are forwarded, e.g. ./run.sh --observe_sleep 0 --cluster '{"ps":[...],"worker":[...]}'
-# The parameter server exits by itself once every worker has finished (no pkill needed).
-cd "$(dirname "$0")"
-python DOWNPOUR.py --job_name "ps" --task_index 0 "$@" &
-python DOWNPOUR.py --job_name "worker" --task_index 0 "$@" &
-python DOWNPOUR.py --job_name "worker" --task_index 1 "$@" &
-wait
+# DOWNPOUR-Easy (local SGD at lr*task_index, global Adagrad): 1 PS + 2 workers.
+# Flags are forwarded to every task (e.g. --cluster '{"ps":[...],"worker":[...]}'); see ../launch_local.sh.
+here="$(cd "$(dirname "$0")" && pwd)"
+cd "$here" && exec bash ../launch_local.sh DOWNPOUR.py 1 2 "$@"

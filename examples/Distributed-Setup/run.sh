@@ -1,8 +1,5 @@
 #!/bin/bash
-# 1 PS + 1 worker, MonitoredTrainingSession.
-# Extra flags are forwarded, e.g. ./run.sh --observe_sleep 0 --cluster '{"ps":[...],"worker":[...]}'
-# The parameter server exits by itself once every worker has finished (no pkill needed).
-cd "$(dirname "$0")"
-python dist_setup.py --job_name "ps" --task_index 0 "$@" &
-python dist_setup.py --job_name "worker" --task_index 0 "$@" &
-wait
+# PS hello world with MonitoredTrainingSession: 1 PS + 1 worker.
+# Flags are forwarded to every task (e.g. --cluster '{"ps":[...],"worker":[...]}'); see ../launch_local.sh.
+here="$(cd "$(dirname "$0")" && pwd)"
+cd "$here" && exec bash ../launch_local.sh dist_setup.py 1 1 "$@"

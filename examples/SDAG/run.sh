@@ -1,9 +1,5 @@
 #!/bin/bash
 # SDAG (synchronous, windowed): 1 PS + 2 workers.
-# Extra flags are forwarded, e.g. ./run.sh --observe_sleep 0 --cluster '{"ps":[...],"worker":[...]}'
-# The parameter server exits by itself once every worker has finished (no pkill needed).
-cd "$(dirname "$0")"
-python dist_cpu_sing_mach_sync.py --job_name "ps" --task_index 0 "$@" &
-python dist_cpu_sing_mach_sync.py --job_name "worker" --task_index 0 "$@" &
-python dist_cpu_sing_mach_sync.py --job_name "worker" --task_index 1 "$@" &
-wait
+# Flags are forwarded to every task (e.g. --cluster '{"ps":[...],"worker":[...]}'); see ../launch_local.sh.
+here="$(cd "$(dirname "$0")" && pwd)"
+cd "$here" && exec bash ../launch_local.sh dist_cpu_sing_mach_sync.py 1 2 "$@"
