@@ -40,6 +40,13 @@ def parse(argv=None):
     return ap.parse_known_args(argv)[0]
 
 
+def _backend_name():
+    """'rccl' for the production path (torch's "nccl" backend is RCCL on ROCm), else the backend."""
+    import torch.distributed as dist
+    b = dist.get_backend() if dist.is_initialized() else (os.environ.get("DTG_BACKEND") or "nccl")
+    return "rccl" if b == "nccl" else b
+
+
 def main(argv=None):
     a = parse(argv)
     import torch
@@ -119,7 +126,7 @@ def main(argv=None):
     if rank == 0:
         config = {"model": conf["model"], "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": conf["seq_len"]}
         config.update({k: v for k, v in conf.items() if k not in config})
-        config.update({"parallelism": f"dp{world}", "allreduce": f"rccl bf16, {a.bucket_mb:g} MB buckets, overlapped"})
+        config.update({"parallelism": f"dp{world}", "allreduce": f"{_backend_name()} bf16, {a.bucket_mb:g} MB buckets, overlapped"})
         print(json.dumps({
             "metric": metric, "value": round(ips, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
