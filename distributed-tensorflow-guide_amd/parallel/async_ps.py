@@ -32,6 +32,45 @@ import torch.distributed as dist
 _GRAD, _DONE, _ELASTIC = 1, 2, 3
 
 
+# gloo moves CPU tensors only for point-to-point; with DTG_BACKEND=gloo DTG_GLOO_DEVICE=cuda (the
+# one-card rehearsal of this GPU path, see parallel/comm.py) device tensors are staged through host
+# memory.  RCCL sends/receives HBM buffers directly; these helpers are then plain dist calls.
+def _staged(t, group):
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _send(t, dst, group=None):
+    dist.send(t.cpu() if _staged(t, group) else t, dst=dst, group=group)
+
+
+def _recv(t, src=None, group=None):
+    if not _staged(t, group):
+        return dist.recv(t, src=src, group=group)
+    h = torch.empty_like(t, device="cpu")
+    peer = dist.recv(h, src=src, group=group)
+    t.copy_(h)
+    return peer
+
+
+class _HostSend:
+    """isend of a host copy; keeps the copy alive until wait()."""
+
+    def __init__(self, t, dst, group):
+        self._h = t.cpu()
+        self._w = dist.isend(self._h, dst=dst, group=group)
+
+    def wait(self):
+        self._w.wait()
+        self._h = None
+
+    def is_completed(self):
+        return self._w.is_completed()
+
+
+def _isend(t, dst, group=None):
+    return _HostSend(t, dst, group) if _staged(t, group) else dist.isend(t, dst=dst, group=group)
+
+
 def _group_payload_grads(flat):
     return [g.grad for g in flat]
 
@@ -68,7 +107,7 @@ class AsyncPSWorker:
 
     def pull(self):
         for buf in _group_payload_params(self.flat):
-            dist.recv(buf, src=self.ps, group=self.pg)
+            _recv(buf, src=self.ps, group=self.pg)
         if self.local_opt is not None:
             # the local optimizer updates the fp32 master: re-seed it from the pulled parameters
             for g in self.flat:
@@ -89,8 +128,8 @@ class AsyncPSWorker:
         grads = self._acc if self._acc is not None else _group_payload_grads(self.flat)
         self._hdr[0] = _GRAD
         self._hdr[1] = self.local_step
-        dist.send(self._hdr, dst=self.ps, group=self.pg)
-        works = [dist.isend(t, dst=self.ps, group=self.pg) for t in grads]
+        _send(self._hdr, dst=self.ps, group=self.pg)
+        works = [_isend(t, dst=self.ps, group=self.pg) for t in grads]
         for w in works:
             w.wait()
         for t in grads:
@@ -104,7 +143,7 @@ class AsyncPSWorker:
     def finish(self):
         self._hdr[0] = _DONE
         self._hdr[1] = self.local_step
-        dist.send(self._hdr, dst=self.ps, group=self.pg)
+        _send(self._hdr, dst=self.ps, group=self.pg)
 
 
 class AsyncPSServer:
@@ -138,7 +177,7 @@ class AsyncPSServer:
         snap = self._snap[w]
         for s, p in zip(snap, _group_payload_params(self.flat)):
             s.copy_(p)
-        self._send_works[w] = [dist.isend(s, dst=w, group=self.pg) for s in snap]
+        self._send_works[w] = [_isend(s, dst=w, group=self.pg) for s in snap]
         self._pulled_version[w] = self.version
 
     def _apply(self, w):
@@ -169,7 +208,7 @@ class AsyncPSServer:
             self._elastic(w)
             return True
         for b in self._recv[w]:
-            dist.recv(b, src=w, group=self.pg)
+            _recv(b, src=w, group=self.pg)
         self._apply(w)
         self._send_params(w)
         return True
@@ -179,7 +218,7 @@ class AsyncPSServer:
         d = alpha * (x_i - x~), x~ += d, send d back (the worker applies x_i -= d)."""
         bufs = self._recv_elastic[w]
         for b in bufs:
-            dist.recv(b, src=w, group=self.pg)
+            _recv(b, src=w, group=self.pg)
         with torch.no_grad():
             for g, b in zip(self.flat, bufs):
                 b.sub_(g.master).mul_(self.elastic_alpha)
@@ -190,7 +229,7 @@ class AsyncPSServer:
         snap = self._snap_elastic[w]
         for s_, b in zip(snap, bufs):
             s_.copy_(b)
-        self._send_works[w] = [dist.isend(s_, dst=w, group=self.pg) for s_ in snap]
+        self._send_works[w] = [_isend(s_, dst=w, group=self.pg) for s_ in snap]
         self.version += 1
         self.updates += 1
         self.per_worker[w] += 1
@@ -237,7 +276,7 @@ class AsyncPSServer:
         live = set(self.workers)
         hdr = torch.zeros(2, dtype=torch.int64, device=self.dev)
         while live:
-            w = dist.recv(hdr, group=self.pg)  # returns the sender's global rank
+            w = _recv(hdr, group=self.pg)  # returns the sender's global rank
             self._hdr[w].copy_(hdr)
             if not self._handle(w):
                 live.discard(w)
@@ -267,7 +306,7 @@ class ElasticWorker:
     def begin(self):
         """Start from the center: receive the PS parameters (mirror / fp32 group) into the replica."""
         for buf in _group_payload_params(self.flat):
-            dist.recv(buf, src=self.ps, group=self.pg)
+            _recv(buf, src=self.ps, group=self.pg)
         with torch.no_grad():
             for g in self.flat:
                 if g.mirror is not None:
@@ -281,12 +320,12 @@ class ElasticWorker:
             return False
         self._hdr[0] = _ELASTIC
         self._hdr[1] = self.local_step
-        dist.send(self._hdr, dst=self.ps, group=self.pg)
-        works = [dist.isend(g.master, dst=self.ps, group=self.pg) for g in self.flat]
+        _send(self._hdr, dst=self.ps, group=self.pg)
+        works = [_isend(g.master, dst=self.ps, group=self.pg) for g in self.flat]
         for w in works:
             w.wait()
         for d in self._d:
-            dist.recv(d, src=self.ps, group=self.pg)
+            _recv(d, src=self.ps, group=self.pg)
         with torch.no_grad():
             for g, d in zip(self.flat, self._d):
                 g.master.sub_(d)
@@ -297,7 +336,7 @@ class ElasticWorker:
     def finish(self):
         self._hdr[0] = _DONE
         self._hdr[1] = self.local_step
-        dist.send(self._hdr, dst=self.ps, group=self.pg)
+        _send(self._hdr, dst=self.ps, group=self.pg)
 
 
 def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1):
@@ -313,10 +352,12 @@ def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1
     n_workers = len(spec["worker"])
     rank = 0 if job_name == "ps" else 1 + int(task_index)
     world = 1 + n_workers
+    backend = os.environ.get("DTG_BACKEND") or backend
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
-    device = torch.device("cuda", 0) if backend == "nccl" else torch.device("cpu")
-    if backend == "nccl":
+    gloo_cuda = backend == "gloo" and os.environ.get("DTG_GLOO_DEVICE") == "cuda" and torch.cuda.is_available()
+    device = torch.device("cuda", 0) if backend == "nccl" or gloo_cuda else torch.device("cpu")
+    if device.type == "cuda":
         torch.cuda.set_device(device)
     os.environ["MASTER_ADDR"] = "127.0.0.1" if ps_host in ("localhost", "") else ps_host
     os.environ["MASTER_PORT"] = str(int(ps_port) + port_offset)
