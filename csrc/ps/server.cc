@@ -139,10 +139,12 @@ void Server::start() {
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_port = htons((uint16_t)port_);
-  if (host_.empty() || host_ == "0.0.0.0" || host_ == "*") {
+  // all interfaces only when asked for explicitly ("0.0.0.0" / "*": a multi-host ClusterSpec); an
+  // unspecified host binds the loopback interface -- the service has no authentication
+  if (host_ == "0.0.0.0" || host_ == "*") {
     a.sin_addr.s_addr = htonl(INADDR_ANY);
   } else {
-    std::string h = host_ == "localhost" ? "127.0.0.1" : host_;
+    std::string h = (host_.empty() || host_ == "localhost") ? "127.0.0.1" : host_;
     if (inet_pton(AF_INET, h.c_str(), &a.sin_addr) != 1) {
       addrinfo hints{}, *res = nullptr;
       hints.ai_family = AF_INET;
@@ -275,7 +277,7 @@ int64_t Server::apply(int64_t opt, const double* hyper, bool locking, const std:
     Tensor g = rd.tensor();
     if (names) names->push_back(name);
     auto v = get_var(name);
-    if (v->dtype != F32 || g.dtype != F32 || g.numel() != v->numel())
+    if (v->dtype != F32 || g.dtype != F32 || g.numel() != v->numel() || g.data.size() != v->data.size())
       throw std::runtime_error("apply: '" + name + "' needs matching float32 gradient");
     float* w = (float*)v->data.data();
     const float* gr = (const float*)g.data.data();
@@ -391,7 +393,8 @@ int32_t Server::dispatch(uint16_t op, Reader& rd, Writer& wr) {
         const std::string name = rd.str();
         Tensor t = rd.tensor();
         auto v = get_var(name);
-        if (t.data.size() != v->data.size()) throw std::runtime_error("assign: size mismatch for " + name);
+        if (t.data.size() != v->data.size() || t.dtype != v->dtype)
+          throw std::runtime_error("assign: size/dtype mismatch for " + name);
         std::lock_guard<std::mutex> g(v->mu);
         uint32_t* d = (uint32_t*)v->data.data();
         const uint32_t* s = (const uint32_t*)t.data.data();
@@ -472,7 +475,8 @@ int32_t Server::dispatch(uint16_t op, Reader& rd, Writer& wr) {
       Tensor g = rd.tensor();
       auto a = get_acc(name, false);
       std::lock_guard<std::mutex> lk(a->mu);
-      if (g.dtype != F32 || (size_t)g.numel() != a->sum.size()) throw std::runtime_error("acc_apply: shape mismatch");
+      if (g.dtype != F32 || (size_t)g.numel() != a->sum.size() || g.data.size() != a->sum.size() * 4)
+        throw std::runtime_error("acc_apply: shape mismatch");
       if (local_step < a->global_step) {  // stale gradient: dropped (ConditionalAccumulator)
         a->dropped++;
         wr.i64(0);

@@ -75,9 +75,19 @@ def _group_payload_grads(flat):
     return [g.grad for g in flat]
 
 
+def _buffers(flat):
+    fb = getattr(flat, "buffers", None)
+    return [fb.flat] if fb is not None else []
+
+
 def _group_payload_params(flat):
-    # what the model reads: the bf16 mirror of the compute group, the fp32 master of the fp32 group
-    return [g.mirror if g.mirror is not None else g.master for g in flat]
+    # what the model reads: the bf16 mirror of the compute group, the fp32 master of the fp32 group,
+    # and the module buffers (BN running statistics: PS variables in the reference's TF setup)
+    return [g.mirror if g.mirror is not None else g.master for g in flat] + _buffers(flat)
+
+
+def _elastic_state(flat):
+    return [g.master for g in flat] + _buffers(flat)
 
 
 class AsyncPSWorker:
@@ -97,6 +107,10 @@ class AsyncPSWorker:
         self.dev = dev
         self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
         self._acc = [torch.zeros_like(g.grad) for g in flat] if (self.window > 1 and local_optimizer) else None
+        # module buffers as pulled: the push carries (current - pulled), the worker's running-statistics
+        # update since the pull, which the PS adds to its own copy
+        self._buf0 = [torch.empty_like(b) for b in _buffers(flat)]
+        self._bufd = [torch.empty_like(b) for b in _buffers(flat)]
         self.local_step = 0
         self.pushes = 0
 
@@ -108,6 +122,8 @@ class AsyncPSWorker:
     def pull(self):
         for buf in _group_payload_params(self.flat):
             _recv(buf, src=self.ps, group=self.pg)
+        for b0, b in zip(self._buf0, _buffers(self.flat)):
+            b0.copy_(b)
         if self.local_opt is not None:
             # the local optimizer updates the fp32 master: re-seed it from the pulled parameters
             for g in self.flat:
@@ -126,10 +142,12 @@ class AsyncPSWorker:
         if self.local_step % self.window:
             return False
         grads = self._acc if self._acc is not None else _group_payload_grads(self.flat)
+        for d, b, b0 in zip(self._bufd, _buffers(self.flat), self._buf0):
+            torch.sub(b, b0, out=d)
         self._hdr[0] = _GRAD
         self._hdr[1] = self.local_step
         _send(self._hdr, dst=self.ps, group=self.pg)
-        works = [_isend(t, dst=self.ps, group=self.pg) for t in grads]
+        works = [_isend(t, dst=self.ps, group=self.pg) for t in list(grads) + self._bufd]
         for w in works:
             w.wait()
         for t in grads:
@@ -161,6 +179,7 @@ class AsyncPSServer:
         dev = next(iter(flat)).master.device
         self.dev = dev
         self._recv = {w: [torch.empty_like(g.grad) for g in flat] for w in self.workers}
+        self._recv_buf = {w: [torch.empty_like(b) for b in _buffers(flat)] for w in self.workers}
         self._snap = {w: [torch.empty_like(t) for t in _group_payload_params(flat)] for w in self.workers}
         self._hdr = {w: torch.zeros(2, dtype=torch.int64, device=dev) for w in self.workers}
         self._send_works = {w: [] for w in self.workers}
@@ -192,6 +211,10 @@ class AsyncPSServer:
         finally:
             for g, s in zip(self.flat, saved):
                 g.grad = s
+        # running statistics: add the worker's update since its pull (lock-free, Hogwild-style, like the
+        # reference's unlocked assign_moving_average on PS variables)
+        for b, d in zip(_buffers(self.flat), self._recv_buf[w]):
+            b.add_(d)
         if self.staleness is not None:
             self.staleness.append(tau)
             self.scales.append(scale)
@@ -207,7 +230,7 @@ class AsyncPSServer:
         if kind == _ELASTIC:
             self._elastic(w)
             return True
-        for b in self._recv[w]:
+        for b in self._recv[w] + self._recv_buf[w]:
             _recv(b, src=w, group=self.pg)
         self._apply(w)
         self._send_params(w)
@@ -220,9 +243,10 @@ class AsyncPSServer:
         for b in bufs:
             _recv(b, src=w, group=self.pg)
         with torch.no_grad():
-            for g, b in zip(self.flat, bufs):
-                b.sub_(g.master).mul_(self.elastic_alpha)
-                g.master.add_(b)
+            for c, b in zip(_elastic_state(self.flat), bufs):
+                b.sub_(c).mul_(self.elastic_alpha)
+                c.add_(b)
+            for g in self.flat:
                 g.refresh_mirror()
         for prev in self._send_works[w]:
             prev.wait()
@@ -237,8 +261,8 @@ class AsyncPSServer:
     def enable_elastic(self, alpha):
         """Serve EASGD exchanges: the PS parameters are the elastic center variable x~."""
         self.elastic_alpha = float(alpha)
-        self._recv_elastic = {w: [torch.empty_like(g.master) for g in self.flat] for w in self.workers}
-        self._snap_elastic = {w: [torch.empty_like(g.master) for g in self.flat] for w in self.workers}
+        self._recv_elastic = {w: [torch.empty_like(t) for t in _elastic_state(self.flat)] for w in self.workers}
+        self._snap_elastic = {w: [torch.empty_like(t) for t in _elastic_state(self.flat)] for w in self.workers}
         return self
 
     def serve(self, poll_sleep=0.0):
@@ -299,7 +323,7 @@ class ElasticWorker:
         self.pg = group
         dev = next(iter(flat)).master.device
         self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
-        self._d = [torch.empty_like(g.master) for g in flat]
+        self._d = [torch.empty_like(t) for t in _elastic_state(flat)]
         self.local_step = 0
         self.exchanges = 0
 
@@ -321,14 +345,15 @@ class ElasticWorker:
         self._hdr[0] = _ELASTIC
         self._hdr[1] = self.local_step
         _send(self._hdr, dst=self.ps, group=self.pg)
-        works = [_isend(g.master, dst=self.ps, group=self.pg) for g in self.flat]
+        works = [_isend(t, dst=self.ps, group=self.pg) for t in _elastic_state(self.flat)]
         for w in works:
             w.wait()
         for d in self._d:
             _recv(d, src=self.ps, group=self.pg)
         with torch.no_grad():
-            for g, d in zip(self.flat, self._d):
-                g.master.sub_(d)
+            for t, d in zip(_elastic_state(self.flat), self._d):
+                t.sub_(d)
+            for g in self.flat:
                 g.refresh_mirror()
         self.exchanges += 1
         return True

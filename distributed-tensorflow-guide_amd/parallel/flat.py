@@ -89,6 +89,42 @@ class FlatGroup:
         self.grad.zero_()
 
 
+class FlatBuffers:
+    """The module's floating-point buffers (BatchNorm running_mean / running_var) in ONE fp32 flat
+    buffer; every module buffer is rebound to a view of it, so kernels that update the statistics in
+    place write straight into the flat storage.  The async PS moves this buffer with the parameters
+    (in TF's between-graph setup the BN moving averages are PS variables the workers update)."""
+
+    def __init__(self, module, device=None):
+        entries = []
+        for mname, m in module.named_modules():
+            for bname, b in m._buffers.items():
+                if b is not None and b.dtype == torch.float32:
+                    entries.append((f"{mname}.{bname}" if mname else bname, m, bname, b))
+        self.names = [e[0] for e in entries]
+        self.offsets = []
+        off = 0
+        for _, _, _, b in entries:
+            self.offsets.append(off)
+            off += _align(b.numel())
+        self.numel = off
+        device = device or (entries[0][3].device if entries else torch.device("cpu"))
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.views = []
+        with torch.no_grad():
+            for (_, m, bname, b), o in zip(entries, self.offsets):
+                v = self.flat[o:o + b.numel()].view(b.shape)
+                v.copy_(b)
+                m._buffers[bname] = v
+                self.views.append(v)
+
+    def __len__(self):
+        return len(self.names)
+
+    def named(self):
+        return zip(self.names, self.views)
+
+
 class FlatParams:
     """Partition a module's parameters into flat groups (see module docstring)."""
 
@@ -107,6 +143,8 @@ class FlatParams:
         if f32:
             self.groups["fp32"] = FlatGroup("fp32", [p for _, p in f32], [n for n, _ in f32], torch.float32, device)
         self.module = module
+        fb = FlatBuffers(module, device)
+        self.buffers = fb if len(fb) else None
 
     def __iter__(self):
         return iter(self.groups.values())

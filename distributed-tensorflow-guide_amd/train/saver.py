@@ -241,11 +241,13 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
     for n, b in flat.module.named_buffers():
         arrays.append((n, _np_of(b)))
     if optimizer is not None:
+        from ..parallel.flat import _view_like
         for g in flat:
             for k, buf in g.state.items():
                 for i, n in enumerate(g.names):
-                    o, numel = g.offsets[i], g.params[i].numel()
-                    arrays.append(("%s/%s" % (n, k), _np_of(buf[o:o + numel].view(g.params[i].shape))))
+                    # same logical layout as the master (channels_last conv weights included), so
+                    # '<param>/<slot>' is element-aligned with '<param>' for any reader
+                    arrays.append(("%s/%s" % (n, k), _np_of(_view_like(buf, g.offsets[i], g.params[i]))))
     if global_step is not None:
         arrays.append(("global_step", np.array(int(global_step), dtype=np.int64)))
         prefix = "%s-%d" % (prefix, int(global_step))
@@ -267,6 +269,7 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
 
 
 def restore_flat(flat, prefix, optimizer=None):
+    from ..parallel.flat import _view_like
     vals = read_tensors(prefix)
     with torch.no_grad():
         for g in flat:
@@ -276,8 +279,8 @@ def restore_flat(flat, prefix, optimizer=None):
                 for k, buf in g.state.items():
                     key = "%s/%s" % (n, k)
                     if key in vals:
-                        o, numel = g.offsets[i], g.params[i].numel()
-                        buf[o:o + numel].copy_(torch.from_numpy(vals[key]).view(-1))
+                        sv = _view_like(buf, g.offsets[i], g.params[i])
+                        sv.copy_(torch.from_numpy(vals[key]).view(sv.shape))
             g.refresh_mirror()
         for n, b in flat.module.named_buffers():
             if n in vals:

@@ -13,18 +13,20 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _model():
+def _model(bn=False):
     import dtg  # noqa: F401
-    from dtg.models.layers import Linear
+    from dtg.models.layers import BatchNorm2d, Linear
 
     class M(torch.nn.Module):
         def __init__(self):
             super().__init__()
-            self.a = Linear(8, 16, act="relu")
+            self.a = Linear(8, 16, act=None if bn else "relu")
+            self.n = BatchNorm2d(16) if bn else None
             self.b = Linear(16, 3)
 
         def forward(self, x):
-            return self.b(self.a(x))
+            h = self.a(x)
+            return self.b(self.n(h) if self.n is not None else h)
     torch.manual_seed(0)
     return M()
 
@@ -34,7 +36,7 @@ def _data(seed):
     return torch.randn(32, 8, generator=g), torch.randint(0, 3, (32,), generator=g)
 
 
-def _rank(rank, world, port, steps, window, mode, q, dyn=False):
+def _rank(rank, world, port, steps, window, mode, q, dyn=False, bn=False):
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -45,16 +47,18 @@ def _rank(rank, world, port, steps, window, mode, q, dyn=False):
         from dtg.parallel import FlatParams, comm
         from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
         comm.init("gloo")
-        model = _model()
+        model = _model(bn)
         flat = FlatParams(model, compute_dtype=torch.float32)
+        # numpy payloads: torch CPU tensors would travel by fd-sharing, which races the child's exit
+        bufs = lambda: {n: b.clone().numpy() for n, b in model.named_buffers()}  # noqa: E731
         if rank == 0:
             opt = FusedSGD(flat, lr=0.1, momentum=0.0)
             ps = AsyncPSServer(flat, opt, workers=range(1, world), window=window, window_mode=mode,
                                staleness_log=True, staleness_scaling="dyn" if dyn else None)
             n = ps.serve()
             q.put((rank, "ok", {"updates": n, "per_worker": dict(ps.per_worker),
-                                "w": [t.clone() for t in (g.master for g in flat)],
-                                "staleness": list(ps.staleness), "scales": list(ps.scales)}))
+                                "w": [g.master.clone().numpy() for g in flat],
+                                "staleness": list(ps.staleness), "scales": list(ps.scales), "bufs": bufs()}))
         else:
             w = AsyncPSWorker(flat, ps_rank=0, window=window, window_mode=mode)
             w.begin()
@@ -66,7 +70,7 @@ def _rank(rank, world, port, steps, window, mode, q, dyn=False):
                 w.step_done()
                 losses.append(loss.item())
             w.finish()
-            q.put((rank, "ok", {"losses": losses, "pushes": w.pushes}))
+            q.put((rank, "ok", {"losses": losses, "pushes": w.pushes, "bufs": bufs()}))
         comm.shutdown()
     except Exception:  # pragma: no cover
         import traceback
@@ -74,13 +78,13 @@ def _rank(rank, world, port, steps, window, mode, q, dyn=False):
         raise
 
 
-def _run(world, steps, window=1, mode="sum", dyn=False):
+def _run(world, steps, window=1, mode="sum", dyn=False, bn=False):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _cluster import free_ports
     port = free_ports(1)[0]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, steps, window, mode, q, dyn)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, steps, window, mode, q, dyn, bn)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -121,7 +125,7 @@ def _ps_params_by_name(out):
     model = _model()
     flat = FlatParams(model, compute_dtype=torch.float32)
     for g, w in zip(flat, out[0]["w"]):
-        g.master.copy_(w)
+        g.master.copy_(torch.as_tensor(w))
     return dict(flat.named_masters())
 
 
@@ -169,7 +173,7 @@ def _elastic_rank(rank, world, port, steps, tau, alpha, q):
         if rank == 0:
             ps = AsyncPSServer(flat, None, workers=range(1, world)).enable_elastic(alpha)
             n = ps.serve()
-            q.put((rank, "ok", {"updates": n, "w": [g.master.clone() for g in flat]}))
+            q.put((rank, "ok", {"updates": n, "w": [g.master.clone().numpy() for g in flat]}))
         else:
             w = ElasticWorker(flat, FusedSGD(flat, lr=0.1, momentum=0.0), tau=tau)
             w.begin()
@@ -259,3 +263,21 @@ def test_dynsgd_scales_updates_by_staleness():
         assert abs(sc - 1.0 / (tau + 1)) < 1e-12
     # (per-worker losses are not asserted: each worker sees its own shard, so a worker's loss on its
     # shard can rise while the shared model improves on the union)
+
+
+def test_async_ps_carries_bn_running_stats():
+    """BatchNorm running statistics are PS state: the workers' running-mean/var updates
+    reach the PS.  One worker: the PS statistics equal the worker's after every step is pushed; two
+    workers: the PS statistics move away from their initial (0, 1) values."""
+    out = _run(2, steps=6, bn=True)
+    ps = {n: torch.as_tensor(v) for n, v in out[0]["bufs"].items()}
+    wk = {n: torch.as_tensor(v) for n, v in out[1]["bufs"].items()}
+    assert set(ps) == {"n.running_mean", "n.running_var"}
+    for n in ps:
+        assert torch.allclose(ps[n], wk[n], atol=1e-6), n
+    assert ps["n.running_mean"].abs().max() > 1e-3
+    out = _run(3, steps=6, bn=True)
+    assert out[0]["updates"] == 12
+    ps = {n: torch.as_tensor(v) for n, v in out[0]["bufs"].items()}
+    assert ps["n.running_mean"].abs().max() > 1e-3
+    assert (ps["n.running_var"] - 1).abs().max() > 1e-3

@@ -213,3 +213,36 @@ def test_server_join_returns_when_workers_done():
     c.worker_done(1)
     assert srv.join(timeout=2.0)
     c.close()
+
+
+def test_malformed_tensor_payloads_are_rejected(ps):
+    """A tensor whose byte count disagrees with its shape, or a huge byte count that would wrap the
+    reader's bounds check, gets an error status -- no over-read -- and the service stays up."""
+    import socket
+    import struct
+    s, c = ps
+    c.acc_create("acc_m", np.zeros(4, np.float32), 0)
+
+    def request(op, body):
+        k = socket.create_connection(("127.0.0.1", s.port), timeout=10)
+        try:
+            k.sendall(struct.pack("<IHHQ", 0x50475444, op, 0, len(body)) + body)
+            hdr = b""
+            while len(hdr) < 16:
+                chunk = k.recv(16 - len(hdr))
+                assert chunk, "server closed the connection"
+                hdr += chunk
+            _, status, _ = struct.unpack("<IiQ", hdr)
+            return status
+        finally:
+            k.close()
+
+    name = b"acc_m"
+    head = struct.pack("<I", len(name)) + name + struct.pack("<q", 0)
+    short = head + struct.pack("<BBq", 1, 1, 4) + struct.pack("<Q", 4) + b"\0" * 4   # 4 floats, 4 bytes
+    assert request(9, short) != 0
+    wrap = head + struct.pack("<BBq", 1, 1, 4) + struct.pack("<Q", (1 << 64) - 8)    # nb wraps off + nb
+    assert request(9, wrap) != 0
+    good = head + struct.pack("<BBq", 1, 1, 4) + struct.pack("<Q", 16) + np.ones(4, np.float32).tobytes()
+    assert request(9, good) == 0
+    assert c.acc_num("acc_m")[0] == 1
