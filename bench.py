@@ -37,6 +37,11 @@ def parse(argv=None):
     ap.add_argument("--bucket_mb", type=float, default=0.0, help="0: 8 (resnet50) / 25 (bert)")
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--model", default="resnet50")
+    # whole-step hipGraph replay (parallel/graphs.py; one rank only, multi-rank steps keep their RCCL
+    # all-reduce hooks eager).  Off by default: both steps are GPU-bound (ResNet-50 99.4 % kernel-busy),
+    # so replay measured equal for ResNet-50 (11.93k vs 11.97k img/s) and 2 % slower for BERT
+    # (profiles/r02_baselines)
+    ap.add_argument("--graph", type=int, default=0, help="-1 auto (capture where supported), 0 eager, 1 capture")
     return ap.parse_known_args(argv)[0]
 
 
@@ -106,6 +111,11 @@ def main(argv=None):
         metric, unit = METRIC, "images/sec"
         conf = {"model": "ResNet-50", "seq_len": None, "image_size": a.image, "optimizer": "momentum-sgd (fused)"}
 
+    from dtg.parallel import GraphedStep, capture_supported
+    use_graph = (a.graph == 1 or (a.graph == -1 and capture_supported(world))) and device.type == "cuda"
+    if use_graph:
+        # warmup = eager steps on a side stream + the capture; the rest of the warmup replays
+        step = GraphedStep(step, warmup=min(2, max(a.warmup - 1, 1)))
     for _ in range(a.warmup):
         loss = step()
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
@@ -126,11 +136,13 @@ def main(argv=None):
     if rank == 0:
         config = {"model": conf["model"], "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": conf["seq_len"]}
         config.update({k: v for k, v in conf.items() if k not in config})
-        config.update({"parallelism": f"dp{world}", "allreduce": f"{_backend_name()} bf16, {a.bucket_mb:g} MB buckets, overlapped"})
+        config.update({"parallelism": f"dp{world}", "allreduce": f"{_backend_name()} bf16, {a.bucket_mb:g} MB buckets, overlapped",
+                       "step_launch": "hipGraph replay" if use_graph else "eager"})
         print(json.dumps({
             "metric": metric, "value": round(ips, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic", "config": config,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init weights)", "config": config,
             "final_loss": final_loss}), flush=True)
     comm.shutdown()
 

@@ -4,3 +4,4 @@ from .ddp import DataParallel  # noqa: F401
 from . import comm  # noqa: F401
 from .async_ps import AsyncPSServer, AsyncPSWorker  # noqa: F401
 from .strategy import MirroredStrategy  # noqa: F401
+from .graphs import GraphedStep, capture_supported  # noqa: F401
