@@ -69,6 +69,79 @@ Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// ---- fused stem tail (stem.hip) ------------------------------------------------------------------
+void check_chan(const Tensor& t, int64_t C, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C, what,
+              " must be a contiguous fp32 GPU tensor of C elements");
+}
+
+// y [N,H,W,C] (the stem conv output), part: its BN statistics partials (conv_fwd_c8 with_stats)
+// -> (pooled [N,P,Q,C], argmax uint8 [N,P,Q,C], save_mean [C], save_invstd [C]); running stats updated
+std::vector<Tensor> stem_bn_pool_fwd(Tensor y, Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
+                                     double momentum, double eps, int64_t k, int64_t s, int64_t pad) {
+  check_nhwc8(y, "y");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
+                  part.numel() == (long long)dtg::kBnStatSlots * 2 * C,
+              "part must be the conv epilogue's [slots][2][C] fp32 partials");
+  check_chan(gamma, C, "gamma");
+  check_chan(beta, C, "beta");
+  check_chan(rmean, C, "running_mean");
+  check_chan(rvar, C, "running_var");
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && pad >= 0 && pad < k, "unsupported pooling window");
+  TORCH_CHECK(y.numel() / 8 < (1LL << 31), "stem kernels index 16-byte vectors with 32-bit math");
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "empty output");
+  c10::DeviceGuard dg(y.device());
+  auto fopt = y.options().dtype(at::kFloat);
+  auto out = at::empty({N, P, Q, C}, y.options());
+  auto idx = at::empty({N, P, Q, C}, y.options().dtype(at::kByte));
+  auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt), coef = at::empty({2LL * C}, fopt);
+  dtg::stem_bn_pool_fwd(cbfp(y), part.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                        rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
+                        coef.data_ptr<float>(), bfp(out), idx.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s, (int)pad,
+                        P, Q, (float)momentum, (float)eps, cur_stream());
+  return {out, idx, smean, sinv};
+}
+
+// dout [N,P,Q,C], idx, y [N,H,W,C] -> dy [N,H,W,C] (gradient of the stem conv output); dgamma/dbeta
+// accumulated into the given fp32 buffers when both are passed, else returned fresh
+std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor gamma, Tensor beta, Tensor smean,
+                                     Tensor sinv, int64_t k, int64_t s, int64_t pad,
+                                     c10::optional<Tensor> dgamma_acc, c10::optional<Tensor> dbeta_acc) {
+  check_nhwc8(dout, "dout");
+  check_nhwc8(y, "y");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dout.sizes() && idx.is_contiguous(),
+              "idx must be uint8 shaped like dout");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  TORCH_CHECK(dout.size(0) == N && dout.size(1) == P && dout.size(2) == Q && dout.size(3) == C,
+              "dout shape does not match the pooled geometry of y");
+  TORCH_CHECK(y.numel() / 8 < (1LL << 31), "stem kernels index 16-byte vectors with 32-bit math");
+  TORCH_CHECK(k <= 2 * s && pad < k, "stem backward gathers at most 2x2 windows per pixel (k <= 2*stride)");
+  for (auto* t : {&gamma, &beta, &smean, &sinv}) check_chan(*t, C, "per-channel tensor");
+  const bool acc = dgamma_acc.has_value() && dgamma_acc->defined() && dbeta_acc.has_value() && dbeta_acc->defined();
+  c10::DeviceGuard dg(y.device());
+  auto fopt = y.options().dtype(at::kFloat);
+  Tensor dgamma, dbeta;
+  if (acc) {
+    dgamma = *dgamma_acc;
+    dbeta = *dbeta_acc;
+    check_chan(dgamma, C, "dgamma accumulator");
+    check_chan(dbeta, C, "dbeta accumulator");
+  } else {
+    dgamma = at::empty({C}, fopt);
+    dbeta = at::empty({C}, fopt);
+  }
+  auto dy = at::empty_like(y);
+  auto ws = at::empty({dtg::stem_bwd_workspace_floats((long long)N * H * W, C)}, fopt);
+  dtg::stem_bn_pool_bwd(cbfp(dout), idx.data_ptr<uint8_t>(), cbfp(y), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                        smean.data_ptr<float>(), sinv.data_ptr<float>(), bfp(dy), dgamma.data_ptr<float>(),
+                        dbeta.data_ptr<float>(), acc ? 1 : 0, ws.data_ptr<float>(), N, H, W, C, (int)k, (int)s,
+                        (int)pad, P, Q, cur_stream());
+  return {dy, dgamma, dbeta};
+}
+
 // x [N,H,W,C] (any C) -> cols [N*P*Q, Kp] bf16, Kp >= R*S*C, multiple of 8
 Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(), "x NHWC bf16");
@@ -102,6 +175,11 @@ void register_pool_ops(pybind11::module_& m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("stem_bn_pool_fwd", &stem_bn_pool_fwd);
+  m.def("stem_bn_pool_bwd", &stem_bn_pool_bwd, pybind11::arg("dout"), pybind11::arg("idx"), pybind11::arg("y"),
+        pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("smean"), pybind11::arg("sinv"),
+        pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("pad"), pybind11::arg("dgamma_acc") = pybind11::none(),
+        pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("im2col", &im2col);
   m.def("col2im", &col2im);
 }

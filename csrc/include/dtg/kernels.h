@@ -147,6 +147,19 @@ void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H,
 void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
 void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// ---- fused ResNet stem tail: BN (conv-epilogue statistics) + ReLU + max-pool (stem.hip) ----------
+// fwd: finalize the BN statistics (coef = 2C floats: scale, shift; running stats updated) and write the
+//      pooled output + window argmax in one pass over y [N,H,W,C].
+// bwd: dy = BN-backward(relu-mask * maxpool-backward(dout)) without materialising either intermediate;
+//      ws = stem_bwd_workspace_floats(N*H*W, C); dgamma/dbeta overwritten (accum = 0) or accumulated.
+void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, const float* beta, float* rmean,
+                      float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
+                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st);
+long long stem_bwd_workspace_floats(long long M, int C);
+void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
+                      const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
+                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st);
+
 // ---- im2col / col2im, NHWC (im2col.hip) --------------------------------------------------------
 void im2col(const bf16_t* x, bf16_t* cols, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,
             hipStream_t st);

@@ -1,0 +1,304 @@
+// ResNet-50 stem tail, fused: BatchNorm -> ReLU -> 3x3/2 max-pool on the 7x7/2 conv's output
+// y [N, 112, 112, 64] (NHWC bf16), the largest activation of the network (411 MB at batch 256).
+//
+// Unfused, the tail streams y five times and writes two more full-size tensors:
+//   fwd  stats(y) ; apply(y) -> a ; maxpool(a) -> out, idx                     (read y 2x, a 1x, write a)
+//   bwd  maxpool_bwd(dout, idx) -> da ; reduce(da, a, y) ; dx(da, a, y) -> dy   (write da, read da/a/y 2x)
+// Fused:
+//   fwd  the statistics come from the conv's epilogue (bn_epi.cuh mode 1); ONE pass reads y, applies
+//        scale/shift + ReLU in registers and max-pools: a never exists.
+//   bwd  the pre-pool gradient is never stored either: both passes recompute it per input pixel as a
+//        gather over the <= ceil(k/s)^2 pooled outputs whose window covers the pixel (their saved
+//        argmax must point back at it), masked by relu'(bn(y)) recomputed from y and the saved
+//        statistics.  Pass 1 reduces sum(dp), sum(dp*xhat) per channel (chunk partials -> the
+//        deterministic BN finalize), pass 2 writes dy = a*dp + bx*y + c0 for the conv's wgrad.
+// Bytes at batch 256: fwd 411 MB in + 154 MB out (was ~1.8 GB), bwd 2 x (154 + 411) MB in + 411 MB out
+// (was ~2.6 GB).
+//
+// Tie semantics equal the unfused path: values are rounded to bf16 (what apply would have stored)
+// before the window comparison, and the first maximum in window order wins.
+#include "dtg/common.h"
+#include "dtg/kernels.h"
+#include "dtg/bn_finalize.cuh"
+#include "dtg/mfma_gemm.cuh"  // gemm::FastDiv
+
+namespace dtg {
+
+struct StemGeom {
+  int N, H, W, C, P, Q, k, s, pad;
+  gemm::FastDiv fW, fH;
+};
+
+__device__ __forceinline__ float bn_relu_bf(float y, float sc, float sf) {
+  return bf2f(f2bf(fmaxf(fmaf(y, sc, sf), 0.f)));
+}
+
+// ---- forward: out[n,p,q,c] = max over the window of bf16(relu(y*scale + shift)), idx = argmax ----
+// KT > 0: the window size as a compile-time constant: the KT*KT loads are unrolled with clamped
+// addresses and a validity flag (all in flight together).  KT = 0: runtime g.k (the one launched).
+template <int KT>
+__global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                            bf16_t* __restrict__ out, uint8_t* __restrict__ idx,
+                                                            StemGeom g) {
+  const unsigned c8n = g.C >> 3;
+  const unsigned total = (unsigned)g.N * g.P * g.Q * c8n;  // < 2^31 (host check)
+  const int K = KT > 0 ? KT : g.k;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % c8n);
+    unsigned t = i / c8n;
+    const int q = (int)(t % (unsigned)g.Q);
+    t /= (unsigned)g.Q;
+    const int p = (int)(t % (unsigned)g.P);
+    const int n = (int)(t / (unsigned)g.P);
+    float sc[8], sf[8], m[8];
+    load8_f32(coef + c8 * 8, sc);
+    load8_f32(coef + g.C + c8 * 8, sf);
+    uint8_t am[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m[k] = -INFINITY;
+      am[k] = 0;
+    }
+    const int h0 = p * g.s - g.pad, w0 = q * g.s - g.pad;
+    const bf16_t* yn = y + (long long)n * g.H * g.W * g.C + c8 * 8;
+#pragma unroll
+    for (int r = 0; r < (KT > 0 ? KT : 1); ++r) {
+      for (int rr = (KT > 0 ? r : 0); rr < (KT > 0 ? r + 1 : K); ++rr) {
+        const int h = h0 + rr;
+        const bool hok = (unsigned)h < (unsigned)g.H;
+#pragma unroll
+        for (int c = 0; c < (KT > 0 ? KT : 1); ++c) {
+          for (int cc = (KT > 0 ? c : 0); cc < (KT > 0 ? c + 1 : K); ++cc) {
+            const int w = w0 + cc;
+            const bool ok = hok && (unsigned)w < (unsigned)g.W;
+            float v[8];
+            load8_bf16(yn + ((long long)(hok ? h : 0) * g.W + (ok ? w : 0)) * g.C, v);
+            const uint8_t wi = (uint8_t)(rr * K + cc);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float a = ok ? bn_relu_bf(v[k], sc[k], sf[k]) : -INFINITY;
+              if (a > m[k]) {  // strict: the first maximum in window order wins ties
+                m[k] = a;
+                am[k] = wi;
+              }
+            }
+          }
+        }
+      }
+    }
+    const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c8 * 8;
+    store8_bf16(out + o, m);
+    uint2 pk;
+    pk.x = am[0] | (am[1] << 8) | (am[2] << 16) | ((uint32_t)am[3] << 24);
+    pk.y = am[4] | (am[5] << 8) | (am[6] << 16) | ((uint32_t)am[7] << 24);
+    *reinterpret_cast<uint2*>(idx + o) = pk;
+  }
+}
+
+// dp at input pixel m = (n, h, w), channels c0..c0+7: sum of the pooled gradients routed to it,
+// masked by relu'(bn(y)) (yv = y at the pixel, sc/sf = the forward scale/shift).  With k <= 2s (the
+// host checks it) a pixel lies in at most 2 x 2 windows: the pooled rows p_hi - 1, p_hi and columns
+// q_hi - 1, q_hi.  All four candidates are loaded unconditionally (clamped addresses, invalid ones
+// masked by an impossible window index) so their loads are independent and in flight together.
+__device__ __forceinline__ void stem_dp(const bf16_t* __restrict__ dout, const uint8_t* __restrict__ idx,
+                                        const StemGeom& g, long long m, int c0, const float (&yv)[8],
+                                        const float (&sc)[8], const float (&sf)[8], float (&dp)[8]) {
+  uint32_t nh, w, n, h;
+  g.fW.divmod((uint32_t)m, nh, w);
+  g.fH.divmod(nh, n, h);
+  const int hp = (int)h + g.pad, wp = (int)w + g.pad;
+  const int p_lo = hp >= g.k ? (hp - g.k) / g.s + 1 : 0, p_hi = min(g.P - 1, hp / g.s);
+  const int q_lo = wp >= g.k ? (wp - g.k) / g.s + 1 : 0, q_hi = min(g.Q - 1, wp / g.s);
+  uint2 pk[4];
+  uint4 dv[4];  // raw bf16 pairs: 16 VGPRs instead of 32 (occupancy of the latency-bound gather)
+  uint32_t wi[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = p_hi - 1 + (j >> 1), q = q_hi - 1 + (j & 1);
+    const bool ok = p >= p_lo && q >= q_lo;  // (p, q <= hi by construction; lo >= 0)
+    const int pc = ok ? p : p_hi, qc = ok ? q : q_hi;
+    wi[j] = ok ? (uint32_t)((hp - p * g.s) * g.k + (wp - q * g.s)) : 0xffu;  // 0xff: matches no index
+    const long long o = (((long long)n * g.P + pc) * g.Q + qc) * g.C + c0;
+    pk[j] = *reinterpret_cast<const uint2*>(idx + o);
+    dv[j] = *reinterpret_cast<const uint4*>(dout + o);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t word = k < 4 ? pk[j].x : pk[j].y;
+      const uint32_t pair = (k >> 1) == 0 ? dv[j].x : (k >> 1) == 1 ? dv[j].y : (k >> 1) == 2 ? dv[j].z : dv[j].w;
+      const float d = __uint_as_float((k & 1) ? (pair & 0xffff0000u) : (pair << 16));
+      acc += ((word >> (8 * (k & 3))) & 0xffu) == wi[j] ? d : 0.f;
+    }
+    dp[k] = fmaf(yv[k], sc[k], sf[k]) > 0.f ? acc : 0.f;
+  }
+}
+
+// ---- backward pass 1: per-chunk sum(dp), sum(dp * xhat) ------------------------------------------
+template <int TPR>
+__global__ void __launch_bounds__(kBlk) stem_bwd_reduce_kernel(const bf16_t* __restrict__ dout,
+                                                               const uint8_t* __restrict__ idx,
+                                                               const bf16_t* __restrict__ y,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta,
+                                                               const float* __restrict__ smean,
+                                                               const float* __restrict__ sinv, StemGeom g, long long M,
+                                                               long long rpc, float* __restrict__ part) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  __shared__ float sh[2][RPP][CW + 4];
+  const int C = g.C;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < C) {
+    float mu[8], is[8], ga[8], be[8], sc[8], sf[8];
+    load8_f32(smean + c0, mu);
+    load8_f32(sinv + c0, is);
+    load8_f32(gamma + c0, ga);
+    load8_f32(beta + c0, be);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = ga[k] * is[k];
+      sf[k] = be[k] - mu[k] * sc[k];
+    }
+    const long long m0 = (long long)blockIdx.x * rpc;
+    const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+    for (long long m = m0 + ty; m < m1; m += RPP) {
+      float yv[8], dp[8];
+      load8_bf16(y + m * C + c0, yv);
+      stem_dp(dout, idx, g, m, c0, yv, sc, sf, dp);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += dp[k];
+        q[k] += dp[k] * (yv[k] - mu[k]) * is[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sh[0][ty][tx * 8 + k] = s[k];
+    sh[1][ty][tx * 8 + k] = q[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < CW; c += kBlk) {
+    float ts = 0.f, tq = 0.f;
+#pragma unroll 4
+    for (int r = 0; r < RPP; ++r) {
+      ts += sh[0][r][c];
+      tq += sh[1][r][c];
+    }
+    const int cc = blockIdx.y * CW + c;
+    if (cc < C) {
+      part[((long long)blockIdx.x * 2 + 0) * C + cc] = ts;
+      part[((long long)blockIdx.x * 2 + 1) * C + cc] = tq;
+    }
+  }
+}
+
+// ---- backward pass 2: dy = a*dp + bx*y + c0 ------------------------------------------------------
+template <int TPR>
+__global__ void __launch_bounds__(kBlk) stem_bwd_dx_kernel(const bf16_t* __restrict__ dout,
+                                                           const uint8_t* __restrict__ idx,
+                                                           const bf16_t* __restrict__ y, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ smean,
+                                                           const float* __restrict__ sinv,
+                                                           const float* __restrict__ coef, StemGeom g, long long M,
+                                                           long long rpc, bf16_t* __restrict__ dy) {
+  constexpr int RPP = kBlk / TPR, CW = TPR * 8;
+  const int C = g.C;
+  const int tx = threadIdx.x % TPR, ty = threadIdx.x / TPR;
+  const int c0 = blockIdx.y * CW + tx * 8;
+  if (c0 >= C) return;
+  float sc[8], sf[8], a[8], bx[8], cc[8];
+  {
+    float mu[8], is[8], ga[8], be[8];
+    load8_f32(smean + c0, mu);
+    load8_f32(sinv + c0, is);
+    load8_f32(gamma + c0, ga);
+    load8_f32(beta + c0, be);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = ga[k] * is[k];
+      sf[k] = be[k] - mu[k] * sc[k];
+    }
+  }
+  load8_f32(coef + c0, a);
+  load8_f32(coef + C + c0, bx);
+  load8_f32(coef + 2 * C + c0, cc);
+  const long long m0 = (long long)blockIdx.x * rpc;
+  const long long m1 = m0 + rpc < M ? m0 + rpc : M;
+  for (long long m = m0 + ty; m < m1; m += RPP) {
+    float yv[8], dp[8], o[8];
+    load8_bf16(y + m * C + c0, yv);
+    stem_dp(dout, idx, g, m, c0, yv, sc, sf, dp);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], dp[k], fmaf(bx[k], yv[k], cc[k]));
+    store8_bf16(dy + m * C + c0, o);
+  }
+}
+
+static StemGeom stem_geom(int N, int H, int W, int C, int k, int s, int pad, int P, int Q) {
+  StemGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.k = k; g.s = s; g.pad = pad;
+  g.fW = gemm::FastDiv((uint32_t)W);
+  g.fH = gemm::FastDiv((uint32_t)H);
+  return g;
+}
+
+// The gather passes are latency-bound (dependent index math and up to 8 small loads per row), so the
+// reduction runs on ~4x the row chunks of a plain BN reduction (1024 workgroups = 4 per CU); the
+// finalize reads the extra partials once.
+static BnGeom stem_reduce_geom(long long M, int C) {
+  BnGeom g = bn_geom(M, C);
+  const int rpp = kBlk / g.tpr;
+  long long nc = 1024 / g.gy;
+  const long long max_chunks = (M + rpp - 1) / rpp;
+  if (nc > max_chunks) nc = max_chunks;
+  if (nc < 1) nc = 1;
+  g.rows_per_chunk = (M + nc - 1) / nc;
+  g.nchunk = (int)((M + g.rows_per_chunk - 1) / g.rows_per_chunk);
+  return g;
+}
+
+long long stem_bwd_workspace_floats(long long M, int C) {
+  const BnGeom g = stem_reduce_geom(M, C);
+  return (long long)g.nchunk * 2 * C + 3LL * C;
+}
+
+void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, const float* beta, float* rmean,
+                      float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
+                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st) {
+  const long long M = (long long)N * H * W;
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+                                                         sinv, momentum, eps, coef, nullptr, nullptr, 0);
+  const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
+  const long long total = (long long)N * P * Q * (C / 8);
+  // KT = 0 (runtime window loop): the unrolled KT = 3 instance measured slower (240 vs 163 us at batch 256:
+  // nine 16-B loads in flight per lane cost more occupancy than they buy)
+  hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+}
+
+void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
+                      const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
+                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st) {
+  const long long M = (long long)N * H * W;
+  const BnGeom bg = stem_reduce_geom(M, C);
+  const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
+  float* part = ws;
+  float* coef = ws + (long long)bg.nchunk * 2 * C;
+  dim3 grid(bg.nchunk, bg.gy);
+  DTG_TPR_SWITCH(bg.tpr, stem_bwd_reduce_kernel<T><<<grid, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, g, M,
+                                                                         bg.rows_per_chunk, part));
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, bg.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+                                                         nullptr, const_cast<float*>(smean), const_cast<float*>(sinv),
+                                                         0.f, 0.f, coef, dgamma, dbeta);
+  const long long rpa = elementwise_rpc(bg, M);
+  dim3 ga((unsigned)((M + rpa - 1) / rpa), bg.gy);
+  DTG_TPR_SWITCH(bg.tpr, stem_bwd_dx_kernel<T><<<ga, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, coef, g, M,
+                                                                   rpa, dy));
+}
+
+}  // namespace dtg

@@ -50,8 +50,11 @@ class ResNet(nn.Module):
         self.fc = Linear(cin, num_classes, init_std=0.01)
 
     def forward(self, x):
-        x = self.stem(x)
-        x = max_pool2d(x, 3, 2, 1)
+        if resnet_fused.stem_ok(self.stem, x):  # conv + BN + ReLU + max-pool as one node (stem.hip)
+            x = resnet_fused.stem_pool(self.stem, x)
+        else:
+            x = self.stem(x)
+            x = max_pool2d(x, 3, 2, 1)
         x = self.blocks(x)
         x = global_avg_pool(x)
         return self.fc(x)

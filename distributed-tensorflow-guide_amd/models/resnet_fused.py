@@ -32,6 +32,7 @@ mask.
 import os
 
 import torch
+import torch.nn.functional as F
 
 from ..ops._native import lib
 from ..ops.gemm import gemm
@@ -291,3 +292,73 @@ def bottleneck(blk, x):
     if holder and holder[0] is not None:
         y._dtg_bn3 = holder[0]
     return y
+
+
+# ---- stem: 7x7/2 conv (8-channel padded input) -> BN -> ReLU -> 3x3/2 max-pool, one autograd node ------
+# csrc/kernels/stem.hip: the BN statistics come from the conv epilogue, BN+ReLU+pool is one pass over the
+# conv output, and the backward recomputes the pre-pool gradient inside both BN-backward passes, so
+# neither the BN output nor the pre-pool gradient (411 MB each at batch 256) is ever written.
+# DTG_STEM_FUSE=0 restores conv -> BN -> max-pool as separate ops (A/B runs).
+_STEM = os.environ.get("DTG_STEM_FUSE", "1") != "0"
+_POOL = (3, 2, 1)  # ResNet's stem max-pool: 3x3, stride 2, pad 1
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, stem, w, gamma, beta):
+        L = lib()
+        n, c, h, wd = x.shape
+        conv, bn = stem.conv, stem.bn
+        k, _, r, s = w.shape
+        st, pad = conv.stride, conv.padding
+        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous()   # [N, H, W, 8]
+        w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
+        kp = (r * s * 8 + 63) // 64 * 64
+        w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()           # [K, Kp], (r, s, c) columns
+        y4, part = L.conv_fwd_c8(x8, w8, r, s, st, pad, True)      # + BN statistics in the epilogue
+        out, idx, smean, sinv = L.stem_bn_pool_fwd(y4, part, gamma, beta, bn.running_mean, bn.running_var,
+                                                   bn.momentum, bn.eps, *_POOL)
+        ctx.save_for_backward(x8, y4, idx, smean, sinv)
+        ctx.stem = stem
+        ctx.geom = (c, k, r, s, st, pad)
+        return out.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dout):
+        L = lib()
+        x8, y4, idx, smean, sinv = ctx.saved_tensors
+        c, k, r, s, st, pad = ctx.geom
+        stem = ctx.stem
+        w, gamma, beta = stem.conv.weight, stem.bn.weight, stem.bn.bias
+        (dg, dg_direct), (db, db_direct) = _gacc(gamma), _gacc(beta)
+        do4 = dout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
+        dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db)[0]
+        dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
+        L.conv_wgrad(dy4, x8, dw8, 0.0, st, pad)
+        dw = dw8[..., :c].permute(0, 3, 1, 2)                      # [K, C, R, S] view
+        grads = []
+        if grad_sink.enabled(w):
+            w.grad.add_(dw.to(w.grad.dtype))
+            grad_sink.notify(w)
+            grads.append(None)
+        else:
+            grads.append(dw.to(w.dtype).contiguous(memory_format=torch.channels_last))
+        for p, (a, direct) in ((gamma, (dg, dg_direct)), (beta, (db, db_direct))):
+            if direct:
+                grad_sink.notify(p)
+                grads.append(None)
+            else:
+                grads.append(a.to(p.dtype))
+        return (None, None, *grads)
+
+
+def stem_ok(stem, x):
+    w = stem.conv.weight
+    return (_STEM and stem.training and x.is_cuda and x.dtype == torch.bfloat16 and not x.requires_grad
+            and w.dtype == torch.bfloat16 and x.shape[1] <= 8 and w.shape[0] % 64 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def stem_pool(stem, x):
+    """max_pool2d(relu(bn(conv(x))), 3, 2, 1) for the ResNet stem as one fused autograd node."""
+    return _StemFn.apply(x, stem, stem.conv.weight, stem.bn.weight, stem.bn.bias)

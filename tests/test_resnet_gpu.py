@@ -126,3 +126,40 @@ def test_resnet50_step_matches_reference_direction():
     g = flat.groups["compute"].grad
     assert torch.isfinite(loss).item()
     assert torch.isfinite(g.float()).all().item() and g.float().abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_fused_stem_matches_unfused(flat, monkeypatch):
+    """conv7x7/2 -> BN -> ReLU -> maxpool3x3/2 as one node (csrc/kernels/stem.hip: BN statistics from the
+    conv epilogue, BN+ReLU+pool in one pass, gather-form backward) equals the op-by-op path: output,
+    running statistics and the conv / gamma / beta gradients."""
+    from dtg.models.layers import ConvBN
+    from dtg.models import resnet_fused
+    from dtg.ops.pool import max_pool2d
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(4, 3, 64, 64, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for fused in (False, True):
+        monkeypatch.setattr(resnet_fused, "_STEM", fused)
+        torch.manual_seed(0)
+        stem = ConvBN(3, 64, 7, 2, 3).to(dev)
+        stem.bn.weight.data.uniform_(0.5, 1.5)
+        stem.bn.bias.data.uniform_(-0.3, 0.3)
+        if flat:
+            FlatParams(stem)
+        else:
+            stem.conv.weight.data = stem.conv.weight.data.to(torch.bfloat16)
+        stem.train()
+        assert resnet_fused.stem_ok(stem, x) == fused
+        y = resnet_fused.stem_pool(stem, x) if fused else max_pool2d(stem(x), 3, 2, 1)
+        gy = torch.randn(y.shape, generator=g.manual_seed(7)).to(dev)
+        (y.float() * gy).sum().backward()
+        res.append([t.detach().float().clone() for t in (y, stem.bn.running_mean, stem.bn.running_var,
+                                                          stem.conv.weight.grad, stem.bn.weight.grad,
+                                                          stem.bn.bias.grad)])
+    names = ["out", "running_mean", "running_var", "dW", "dgamma", "dbeta"]
+    for name, a, b in zip(names, *res):
+        assert a.shape == b.shape, name
+        err = ((a - b).norm() / (a.norm() + 1e-6)).item()
+        assert err < 2e-2, (name, err)
