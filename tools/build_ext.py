@@ -17,6 +17,7 @@ import concurrent.futures as cf
 import glob
 import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -44,11 +45,35 @@ def _pybind_include():
     return pybind11.get_include()
 
 
-def _headers_digest():
+_INC = re.compile(rb'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _headers_digest(src=None):
+    """Digest of the project headers a source includes (transitively, quoted includes resolved against
+    csrc/include and the including file's directory); without a source, of every project header."""
     h = hashlib.sha256()
-    for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) +
-                    glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True) +
-                    glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)):
+    if src is None:
+        for p in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) +
+                        glob.glob(os.path.join(CSRC, "**", "*.cuh"), recursive=True)):
+            with open(p, "rb") as f:
+                h.update(p.encode())
+                h.update(f.read())
+        return h.hexdigest()
+    seen, todo = set(), [src]
+    while todo:
+        cur = todo.pop()
+        with open(cur, "rb") as f:
+            body = f.read()
+        for inc in _INC.findall(body):
+            inc = inc.decode()
+            for base in (os.path.join(CSRC, "include"), os.path.dirname(cur)):
+                cand = os.path.normpath(os.path.join(base, inc))
+                if os.path.exists(cand):
+                    if cand not in seen:
+                        seen.add(cand)
+                        todo.append(cand)
+                    break
+    for p in sorted(seen):
         with open(p, "rb") as f:
             h.update(p.encode())
             h.update(f.read())
@@ -58,6 +83,7 @@ def _headers_digest():
 def _compile(src, cmd_prefix, flags, hdr_digest, verbose):
     with open(src, "rb") as f:
         body = f.read()
+    hdr_digest = _headers_digest(src)  # only the headers this source actually includes
     key = hashlib.sha256(body + hdr_digest.encode() + " ".join(cmd_prefix + flags).encode()).hexdigest()[:20]
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
     obj = os.path.join(OBJ, f"{rel}.{key}.o")

@@ -40,6 +40,16 @@ def main():
         out = torch.zeros(M, N, device=dev, dtype=torch.float32)
         fn = lambda: L.gemm(A, False, B, False, out, 1.0, 1.0, None, 0, 0)  # noqa: E731
         fl = 2.0 * M * N * K
+    elif op == "gemm_bn3":  # dgrad GEMM + BN backward partials, relu mask from packed bits, += into out
+        M, N, K = a
+        A = torch.randn(M, K, device=dev, dtype=bf)
+        W = torch.randn(K, N, device=dev, dtype=bf)
+        x = torch.randn(M, N, device=dev, dtype=bf)
+        out = torch.randn(M, N, device=dev, dtype=bf)
+        bits = torch.randint(0, 256, (M, N // 8), device=dev, dtype=torch.uint8)
+        ch = [torch.rand(N, device=dev) + 0.5 for _ in range(4)]
+        fn = lambda: L.gemm_bn(A, W, 3, x, *ch, mask=bits, out=out)  # noqa: E731
+        fl = 2.0 * M * N * K
     elif op in ("gemm_bn2",):
         M, N, K = a
         A = torch.randn(M, K, device=dev, dtype=bf)
