@@ -253,7 +253,8 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor> softmax_xent(Tensor logits, Te
 // out[M,N] = act(alpha * op(A) op(B) + beta*out + bias).  a_kc: A stored [M,K] (else [K,M]);
 // b_kc: B stored [N,K] (else [K,N]).  Row strides are taken from the 2-D tensors.
 void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, double beta,
-          c10::optional<Tensor> bias, int64_t act, int64_t split_k, c10::optional<Tensor> aux, int64_t aux_mode) {
+          c10::optional<Tensor> bias, int64_t act, int64_t split_k, c10::optional<Tensor> aux, int64_t aux_mode,
+          c10::optional<Tensor> colsum) {
   CHECK_CUDA(A);
   CHECK_CUDA(B);
   CHECK_CUDA(out);
@@ -290,6 +291,20 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
     auxp = aux->data_ptr();
   }
   c10::DeviceGuard dg(A.device());
+  if (colsum.has_value() && colsum->defined()) {
+    // fused bias gradient: colsum[n] += sum_m out[m, n] (dgrad layout, bf16 out, plain alpha/beta)
+    CHECK_IN(*colsum);
+    CHECK_DT(*colsum, at::kFloat);
+    TORCH_CHECK(colsum->numel() == N, "colsum must hold N floats");
+    TORCH_CHECK(a_kc && !b_kc && out.scalar_type() == at::kBFloat16 && alpha == 1.0 && beta == 0.0,
+                "colsum epilogue: A [M,K], B [K,N], bf16 out, alpha 1, beta 0");
+    TORCH_CHECK(out.stride(0) % 8 == 0 && N % 8 == 0 && ((uintptr_t)out.data_ptr() % 16) == 0 &&
+                    (bptr == nullptr || ((uintptr_t)bptr % 16) == 0) && (auxp == nullptr || ((uintptr_t)auxp % 16) == 0),
+                "colsum epilogue needs 16-byte aligned rows");
+    dtg::gemm_bf16_colsum(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(out), out.stride(0), M, N, K, bptr, (int)act,
+                          auxp, (int)aux_mode, colsum->data_ptr<float>(), cur_stream());
+    return;
+  }
   int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K, a_kc ? 1 : 0);
   Tensor ws;
   float* wsp = nullptr;
@@ -793,7 +808,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"), pybind11::arg("b_kc"),
         pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,
-        pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0);
+        pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0,
+        pybind11::arg("colsum") = pybind11::none());
   register_transformer_ops(m);
   register_pool_ops(m);
 }

@@ -24,7 +24,10 @@ namespace gemm {
 template <class C, int MODE, class ROWMAP>
 __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                             const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
-  static_assert(MODE >= 1 && MODE <= 4, "BN epilogue mode");  // 4 = mode 3 + a second BN (x2)
+  // 4 = mode 3 + a second BN (x2); 5 = not a BN: the GEMM's own bias/activation/aux epilogue
+  // (epi_store8_fast_act) plus the column sums of the stored output added into bn.part[N] (fp32) --
+  // the bias gradient of the layer whose output gradient this GEMM produces, without a re-read
+  static_assert(MODE >= 1 && MODE <= 5, "BN epilogue mode");
   constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
   static_assert(C::NTH % CPR == 0, "fixed column group per thread");
   static_assert((MODE == 4 ? 3 : 2) * RW * C::BN * 4 <= C::LDS_BYTES, "reduction scratch does not fit the LDS ring");
@@ -54,7 +57,11 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   }
   epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
     const int row = rowmap(m);
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 5) {
+      epi_store8_fast_act(e, row, n, v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += bf2f(f2bf(v[k]));  // sum of what was stored
+    } else if constexpr (MODE == 1) {
       epi_store8_fast(e, row, n, v);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -105,6 +112,20 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   // epilogue_staged ended with a barrier: the LDS ring is free for the column reduction
   lds_float* red = reinterpret_cast<lds_float*>(smem);
   const int r = tid / CPR;
+  if constexpr (MODE == 5) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[r * C::BN + cg * 8 + k] = s[k];
+    __syncthreads();
+    for (int c = tid; c < C::BN; c += C::NTH) {
+      if (bn0 + c < N) {
+        float ts = 0.f;
+#pragma unroll 8
+        for (int j = 0; j < RW; ++j) ts += red[j * C::BN + c];
+        atomicAdd(bn.part + bn0 + c, ts);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     red[r * C::BN + cg * 8 + k] = s[k];

@@ -109,6 +109,11 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st);
 
+// C = act(A * B + bias) (B [K,N], the dgrad layout; aux as in gemm_bf16) and colsum[n] += sum_m C[m, n]
+// in the same epilogue (fp32 atomics; the bias gradient of the layer C is the output gradient of)
+void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
+                      int N, int K, const float* bias, int act, void* aux, int aux_mode, float* colsum, hipStream_t st);
+
 // ---- transformer blocks (transformer.hip) ------------------------------------------------------
 int ln_max_hidden();
 void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* s_out,

@@ -1,8 +1,8 @@
 // Fused multi-head attention for BERT-style encoders (head dim 64, additive key mask,
 // attention-probability dropout from the counter hash), forward and backward, on MFMA.
 //
-// Forward  (grid: [B*nh, S/64], 4 waves; a wave owns 16 query rows):
-//   K and V of the (b, h) are staged once into LDS by LDS-DMA (K row-major/KC, V as k-major MC
+// Forward  (grid: [B*nh, ceil(S/128)], 8 waves; a wave owns 16 query rows, a workgroup 128 queries):
+//   K and V of the (b, h) are staged once per 128 queries (once per head at S = 128) into LDS by LDS-DMA (K row-major/KC, V as k-major MC
 //   tiles read back with ds_read_b64_tr_b16); Q fragments come straight from global memory.  Per
 //   64-key chunk: S = Q K^T (8 MFMA) -> scale + mask -> online softmax (running max / sum per row,
 //   reductions across the 16 lanes that share a row) -> dropout(P) through a per-wave LDS
@@ -63,8 +63,10 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------
+constexpr int kFwdWaves = 8;  // 128 queries per workgroup: K/V of a head staged once at S <= 128
+
 template <int SMAX>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
+__global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                        bf16_t* __restrict__ out, float* __restrict__ lse, int S, int nh,
                                                        float scale, uint32_t th, float dscale, uint32_t seed) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -84,16 +86,20 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
     DenseKC<false> ks_{Kg, ld, S, 64};
     DenseMC<false> vs_{Vg, ld, 64, S};
     for (int c = 0; c < nkc; ++c) {
-      stage_kc<64>(ks_, Kt + c * 8192, c * 64, 0, wave, lane);
-      stage_mc<64>(vs_, Vt + c * 8192, 0, c * 64, wave, lane);
+      stage_kc<64, DenseKC<false>, kFwdWaves>(ks_, Kt + c * 8192, c * 64, 0, wave, lane);
+      stage_mc<64, DenseMC<false>, kFwdWaves>(vs_, Vt + c * 8192, 0, c * 64, wave, lane);
     }
   }
-  const int q0 = blockIdx.y * 64 + wave * 16;
+  const int q0 = blockIdx.y * (16 * kFwdWaves) + wave * 16;
+  const bool active = q0 < S;  // S % 64 == 0: the last workgroup of S = 64 * odd has 4 idle waves
   v8bf qa[2];
-  qa[0] = gfrag(Qg, ld, q0, 0, lane);
-  qa[1] = gfrag(Qg, ld, q0, 1, lane);
+  if (active) {
+    qa[0] = gfrag(Qg, ld, q0, 0, lane);
+    qa[1] = gfrag(Qg, ld, q0, 1, lane);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (!active) return;  // (no barrier below this point)
   const float* mk = mask ? mask + (long long)b * S : nullptr;
   float m[4], l[4];
   f32x4 o[4];
@@ -191,9 +197,11 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const bf16_t* __restrict_
 
 // ---------------------------------------------------------------------------------------------
 // Backward, S in {64, 128}: one workgroup (8 waves) per (b, h); wave w owns keys [16w, 16w+16).
-// LDS (S = 128: 90 KB): Q, dO, K as MC tiles (ds_read_b64_tr_b16 B-operands), the whole dS^T
-// [S keys][S q] bf16 (written by the key-waves, read back transposed for dQ = dS K -- no atomics),
-// D / LSE / mask rows, and per-wave [16 keys][32 q] scratch for dropout(P)^T.
+// LDS (S = 128: 74 KB, so two workgroups share a CU): Q and dO as MC tiles (ds_read_b64_tr_b16
+// B-operands), the whole dS^T [S keys][S q] bf16 (written by the key-waves, read back transposed for
+// dQ = dS K -- no atomics), D / LSE / mask rows, and per-wave [16 keys][32 q] scratch for
+// dropout(P)^T.  K is only read by phase 2, so it is staged into the Q tile after phase 1 (its DMA
+// overlaps the dK / dV stores, which stage through the dO tile).
 //   phase 1 (per 32-query chunk): S^T = K Q^T, dP^T = V dO^T (16 MFMA) -> P^T, dropout, dS^T
 //            -> dV += Pd^T dO, dK += dS^T Q (8 MFMA)
 //   phase 2 (after a barrier): wave w computes dQ for query rows [16w, 16w+16) over all keys.
@@ -239,10 +247,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
   const bf16_t* Vg = Qg + 2 * H;
   const bf16_t* Og = o + (long long)b * S * H + h * 64;
   const bf16_t* dOg = dout + (long long)b * S * H + h * 64;
-  lds_char* Qt = smem;                         // MC [q][d]
-  lds_char* dOt = Qt + S * 128;                // MC [q][d]
-  lds_char* Kt = dOt + S * 128;                // MC [key][d]
-  lds_char* dST = Kt + S * 128;                // [S][S] bf16
+  lds_char* Qt = smem;                         // MC [q][d]; phase 2: K as MC [key][d]
+  lds_char* dOt = Qt + S * 128;                // MC [q][d]; phase 2: per-wave output staging
+  lds_char* Kt = Qt;
+  lds_char* dST = dOt + S * 128;               // [S][S] bf16
   lds_float* Ds = reinterpret_cast<lds_float*>(dST + S * S * 2);
   lds_float* Ls = Ds + S;
   lds_float* Ms = Ls + S;
@@ -250,12 +258,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
   {
     DenseMC<false> qs_{Qg, ld, 64, S};
     DenseMC<false> ds_{dOg, (long long)H, 64, S};
-    DenseMC<false> kss{Kg, ld, 64, S};
 #pragma unroll
     for (int c = 0; c < S / 64; ++c) {
       stage_mc<64, DenseMC<false>, NW>(qs_, Qt + c * 8192, 0, c * 64, wave, lane);
       stage_mc<64, DenseMC<false>, NW>(ds_, dOt + c * 8192, 0, c * 64, wave, lane);
-      stage_mc<64, DenseMC<false>, NW>(kss, Kt + c * 8192, 0, c * 64, wave, lane);
     }
   }
   if (tid < 2 * S) {  // D[q] = sum_d dO[q, d] * O[q, d]: two threads per row
@@ -337,13 +343,20 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
       lds_fence();  // scratch rewritten by the next chunk
     }
   }
-  __syncthreads();  // dS^T complete; Q / dO tiles free for output staging
-  lds_char* stg = smem + wave * 2048;  // inside the Q / dO tiles (16 or 32 KB)
+  __syncthreads();  // dS^T complete; the Q / dO tiles are free
+  {  // K for dQ = dS K into the Q tile: its DMA is in flight while dK / dV are stored
+    DenseMC<false> kss{Kg, ld, 64, S};
+#pragma unroll
+    for (int c = 0; c < S / 64; ++c) stage_mc<64, DenseMC<false>, NW>(kss, Kt + c * 8192, 0, c * 64, wave, lane);
+  }
+  lds_char* stg = dOt + wave * 2048;  // per-wave output staging inside the dO tile (16 or 32 KB)
   if (has_keys) {
     bf16_t* gk = dqkv + ((long long)b * S + kb) * ld + H + h * 64;
     store_rows16(stg, dk, scale, gk, ld, lane);
     store_rows16(stg, dv, 1.f, gk + H, ld, lane);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // K staged by every wave
   const int qr = wave * 16;
   if (qr < S) {
     f32x4 dq[4];
@@ -372,8 +385,8 @@ int attn_fused_supported(int S, int dh, int backward) {
   return backward ? (S == 64 || S == 128) : (S <= 512);
 }
 
-static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + 4 * 2048; }
-static size_t bwd_lds(int S) { return (size_t)3 * S * 128 + (size_t)S * S * 2 + 3 * S * 4 + 8 * 1024; }
+static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + kFwdWaves * 2048; }
+static size_t bwd_lds(int S) { return (size_t)2 * S * 128 + (size_t)S * S * 2 + 3 * S * 4 + 8 * 1024; }
 
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,
               uint32_t seed, hipStream_t st) {
@@ -385,8 +398,8 @@ void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int
   }
   const uint32_t th = drop_th(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  dim3 grid(B * nh, S / 64);
-  hipLaunchKernelGGL(attn_fwd_kernel<512>, grid, dim3(256), fwd_lds(S), st, qkv, mask, out, lse, S, nh, 0.125f, th,
+  dim3 grid(B * nh, (S + 16 * kFwdWaves - 1) / (16 * kFwdWaves));
+  hipLaunchKernelGGL(attn_fwd_kernel<512>, grid, dim3(64 * kFwdWaves), fwd_lds(S), st, qkv, mask, out, lse, S, nh, 0.125f, th,
                      ds, seed);
 }
 

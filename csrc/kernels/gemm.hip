@@ -183,6 +183,11 @@ static bool gemm_rp() {
 // 50176x256x1024 at 204 flop/B is 8 % slower with it).
 static bool use_rp(int M, int N, int kps) {
   if (!gemm_rp()) return false;
+  // ... but only while the grid is short: with more than ~2 rounds of 128x128 tiles (> 2048 at 4 per CU)
+  // the fourth resident workgroup the plain single stage keeps is worth more than in-block pipelining
+  // (BERT-base at 32768 tokens: 32768x3072x768 990 vs 896 TF/s, 32768x2304x768 979 vs 922; at
+  // 1536 tiles the two tie or RP wins -- tools/gemm_ab.py, profiles/r02_gemm)
+  if ((long long)((M + 127) / 128) * ((N + 127) / 128) > 2048) return false;
   if (kps >= 2048) return true;
   const double flop = 2.0 * M * N * kps, bytes = 2.0 * ((double)M * kps + (double)N * kps + (double)M * N);
   return kps >= 768 && flop / bytes >= 300.0;
@@ -307,6 +312,16 @@ void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
   else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.x2) gemm_bn_dispatch<4>(A, lda, B, ldb, M, N, K, e, bn, st);
   else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
+void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
+                      int N, int K, const float* bias, int act, void* aux, int aux_mode, float* colsum, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  Epi e{C, ldc, 1, 1.f, 0.f, bias, act, aux, aux_mode};
+  BnEpi bn;
+  bn.part = colsum;
+  bn.mode = 5;
+  gemm_bn_dispatch<5>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
 }  // namespace dtg

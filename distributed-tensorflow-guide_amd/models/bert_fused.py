@@ -98,8 +98,8 @@ class _LayerFn(torch.autograd.Function):
         ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True, gb_2)  # + db2 = sum(df2)
         gemm(df2, False, f1, False, out=gw_2, beta=1.0)                       # dW2 += df2^T f1
         dpre = torch.empty_like(pre)
-        L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 2)      # df1 * gelu'(pre)
-        L.colsum(dpre, gb_1, True)
+        # df1 * gelu'(pre), and b1's gradient (column sums of it) in the same epilogue
+        L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 2, colsum=gb_1)
         gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                      # dW1 += dpre^T x1
         if p_h <= 0:  # df2 aliases ds2: it has been consumed above; accumulate the residual grad into a copy
             ds2 = ds2.clone()

@@ -39,6 +39,23 @@ def test_gemm_gelu_aux_store_and_grad():
     assert rel(d, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 384, 192), (300, 200, 136)])
+def test_gemm_colsum_epilogue(M, N, K):
+    """Bias gradient fused into the dgrad GEMM epilogue (bn_epi.cuh mode 5): the stored output equals the
+    plain aux-mode-2 GEMM and colsum accumulates its column sums (full and ragged tiles)."""
+    torch.manual_seed(2)
+    dy = torch.randn(M, K, device=dev).bfloat16()
+    w = torch.randn(K, N, device=dev).bfloat16() * 0.1
+    pre = torch.randn(M, N, device=dev).bfloat16()
+    d_ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    lib().gemm(dy, True, w, False, d_ref, 1.0, 0.0, None, 2, 0, pre, 2)
+    d = torch.empty_like(d_ref)
+    cs = torch.full((N,), 0.5, device=dev)  # accumulates onto what is there
+    lib().gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 2, colsum=cs)
+    assert torch.equal(d, d_ref)
+    assert rel(cs - 0.5, d_ref.float().sum(0)) < 1e-4
+
+
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
 def test_gemm_strided_batched(a_kc, b_kc):
     torch.manual_seed(1)

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""In-process A/B of GEMM tile configurations on given shapes (interleaved rounds, one process:
+cdna_hip_programming.md §5.4 rule 24), against torch.matmul (hipBLASLt) on the same random data.
+
+    python tools/gemm_ab.py --shapes 32768x3072x768,32768x768x3072 --cfgs 0,25,99 [--layout nn|nt|tn]
+
+cfg 0 = dtg's heuristic, 25 = register-pipelined 128x128, 99 = 256x256 8-wave 8-phase (gemm8.hip);
+the rest: csrc/kernels/gemm_forced.hip.  Layouts: A [M,K] K-contiguous with B [N,K] (fwd, "nt"),
+B [K,N] (dgrad, "nn"); "tn": A stored [K,M] and B [K,N] (weight gradient, fp32 out).
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import dtg  # noqa: E402,F401
+from dtg.ops._native import lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", required=True)
+    ap.add_argument("--cfgs", default="0,25,99")
+    ap.add_argument("--layout", default="nt")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    L = lib()
+    dev = torch.device("cuda")
+    out = []
+    for shp in a.shapes.split(","):
+        M, N, K = (int(v) for v in shp.split("x"))
+        g = torch.Generator(device="cpu").manual_seed(0)
+        if a.layout == "tn":
+            A = (torch.rand(K, M, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+            B = (torch.rand(K, N, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+            C = torch.zeros(M, N, device=dev, dtype=torch.float32)
+            At, Bt, akc, bkc = A.t(), B, False, False
+        else:
+            A = (torch.rand(M, K, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+            if a.layout == "nt":
+                B = (torch.rand(N, K, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+                Bt, bkc = B.t(), True
+            else:
+                B = (torch.rand(K, N, generator=g) * 2 - 1).to(dev, torch.bfloat16)
+                Bt, bkc = B, False
+            C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            At, akc = A, True
+        Ct = torch.empty(M, N, device=dev, dtype=torch.bfloat16)  # hipBLASLt: bf16 out
+        flops = 2.0 * M * N * K
+        cfgs = [int(c) for c in a.cfgs.split(",")]
+
+        def run_cfg(c):
+            L.gemm_force_cfg(c)
+            L.gemm(A, akc, B, bkc, C, 1.0, 0.0, None, 0, 0)
+
+        times = {c: [] for c in cfgs}
+        times["lib"] = []
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(a.rounds):
+            for c in cfgs + ["lib"]:
+                fn = (lambda: torch.matmul(At, Bt, out=Ct)) if c == "lib" else (lambda c=c: run_cfg(c))
+                fn()
+                torch.cuda.synchronize()
+                s.record()
+                for _ in range(a.iters):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                times[c].append(s.elapsed_time(e) / a.iters * 1e3)
+        L.gemm_force_cfg(0)
+        res = {"shape": shp, "layout": a.layout}
+        for c, ts in times.items():
+            ts.sort()
+            res[str(c)] = {"us_med": round(ts[len(ts) // 2], 1), "us_min": round(ts[0], 1),
+                           "tflops": round(flops / ts[len(ts) // 2] / 1e6, 1)}
+        # correctness of each dtg config against hipBLASLt
+        ref = torch.matmul(At.float(), Bt.float()) if M * N * K <= 2 ** 36 else None
+        if ref is not None:
+            for c in cfgs:
+                run_cfg(c)
+                res[str(c)]["rel_err"] = float(((C.float() - ref).norm() / ref.norm()).item())
+            L.gemm_force_cfg(0)
+        print(json.dumps(res), flush=True)
+        out.append(res)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
