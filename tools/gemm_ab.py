@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
+    ap.add_argument("--splits", default="0", help="comma list of split_k values to try (0 = heuristic)")
     a = ap.parse_args()
     L = lib()
     dev = torch.device("cuda")
@@ -53,11 +54,12 @@ def main():
             At, akc = A, True
         Ct = torch.empty(M, N, device=dev, dtype=torch.bfloat16)  # hipBLASLt: bf16 out
         flops = 2.0 * M * N * K
-        cfgs = [int(c) for c in a.cfgs.split(",")]
+        cfgs = [(int(c), int(sp)) for c in a.cfgs.split(",") for sp in a.splits.split(",")]
 
-        def run_cfg(c):
+        def run_cfg(cs):
+            c, sp = cs
             L.gemm_force_cfg(c)
-            L.gemm(A, akc, B, bkc, C, 1.0, 0.0, None, 0, 0)
+            L.gemm(A, akc, B, bkc, C, 1.0, 0.0, None, 0, sp)
 
         times = {c: [] for c in cfgs}
         times["lib"] = []
@@ -77,6 +79,7 @@ def main():
         res = {"shape": shp, "layout": a.layout}
         for c, ts in times.items():
             ts.sort()
+            c = c if c == "lib" else (f"{c[0]}" if c[1] == 0 else f"{c[0]}/s{c[1]}")
             res[str(c)] = {"us_med": round(ts[len(ts) // 2], 1), "us_min": round(ts[0], 1),
                            "tflops": round(flops / ts[len(ts) // 2] / 1e6, 1)}
         # correctness of each dtg config against hipBLASLt
@@ -84,7 +87,8 @@ def main():
         if ref is not None:
             for c in cfgs:
                 run_cfg(c)
-                res[str(c)]["rel_err"] = float(((C.float() - ref).norm() / ref.norm()).item())
+                key = f"{c[0]}" if c[1] == 0 else f"{c[0]}/s{c[1]}"
+                res[key]["rel_err"] = float(((C.float() - ref).norm() / ref.norm()).item())
             L.gemm_force_cfg(0)
         print(json.dumps(res), flush=True)
         out.append(res)
