@@ -100,7 +100,15 @@ int gemm_pick_split(int M, int N, int K, int a_kc) {
   // forward / data-gradient GEMMs (K-contiguous A) with >= 128 tiles: the fp32 partial round trip
   // costs more than the idle CUs do (BERT 8192x768x3072: 47 us unsplit, 56 us split 2;
   // profiles/r01_rp/sweep_bert.log)
-  if (a_kc && tiles >= 128) return 1;
+  if (a_kc && tiles >= 128) {
+    // ... except a long reduction over a short grid (BERT's MLM decoder dgrad 5120x768x30528: 240
+    // tiles, 834 us unsplit on the 8-phase kernel, 286 us split 2 -- profiles/r02_gemm): split until the
+    // grid is ~1.5 workgroups per CU while each split keeps >= 4096 of K
+    int s = 1;
+    if (K >= 8192)
+      while (tiles * s < 384 && (long long)K / (s * 2) >= 4096) s *= 2;
+    return s;
+  }
   int s = 1;
   // aim for >= ~512 workgroups (2 per CU: the LDS ring admits 2) while keeping >= 1024 K
   // (16 K-steps) per split
@@ -126,12 +134,14 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
 }
 
 // 256x256 / 8-wave / 8-phase kernel (gemm8.hip) for GEMMs big enough to fill the chip with 256x256
-// tiles; DTG_GEMM8=0/1 forces it off/on (A/B runs).
+// tiles.  Opt-in (DTG_GEMM8=1 forces it on, DTG_GEMM8=2 applies the heuristic below): on the only
+// shapes of the flagship steps that reach it, BERT's MLM decoder GEMMs, it lost to the 128x128
+// single-stage kernels (30528x768x5120 wgrad 419 vs 289 us; 5120x768x30528 dgrad 834 vs 286 us split 2;
+// profiles/r02_gemm).
 static bool use_8phase(int M, int N, int K, int split_k) {
-  if (const char* f = getenv("DTG_GEMM8")) {
-    if (f[0] == '0') return false;
-    if (f[0] == '1') return M >= 256 && N >= 128;
-  }
+  const char* f = getenv("DTG_GEMM8");
+  if (!f || f[0] == '0') return false;
+  if (f[0] == '1') return M >= 256 && N >= 128;
   // Both kernels run one "round" of tiles at a time (256x256: 1 workgroup per CU; 128x128: 2 per
   // CU), so compare round utilisation, crediting the 8-phase kernel with its per-CU advantage, which
   // grows with K (measured, profiles/r01_gemm8: ~1.15x at K = 768 in a cold-cache training step, up
