@@ -249,6 +249,31 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor> softmax_xent(Tensor logits, Te
   return {loss, dx, lse};
 }
 
+// dlogits = (softmax(logits) - onehot(labels)) * scale * g, g a 0-d/1-element fp32 GPU tensor (the
+// upstream gradient, read on the device: no host sync, no separate rescale pass)
+Tensor softmax_xent_bwd(Tensor logits, Tensor labels, Tensor lse, Tensor g, double scale) {
+  CHECK_IN(logits);
+  CHECK_IN(labels);
+  CHECK_IN(lse);
+  TORCH_CHECK(logits.dim() == 2, "logits must be [B, V]");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16/fp32");
+  CHECK_DT(labels, at::kLong);
+  CHECK_DT(lse, at::kFloat);
+  const long long B = logits.size(0);
+  const int V = (int)logits.size(1);
+  TORCH_CHECK(labels.numel() == B && lse.numel() == B, "labels / lse size mismatch");
+  CHECK_CUDA(g);
+  TORCH_CHECK(g.numel() == 1, "g must hold one element");
+  Tensor gf = g.scalar_type() == at::kFloat ? g.contiguous() : g.to(at::kFloat);
+  c10::DeviceGuard dg(logits.device());
+  auto dx = at::empty_like(logits);
+  if (B > 0)
+    dtg::softmax_xent_bwd(logits.data_ptr(), logits.scalar_type() == at::kBFloat16,
+                          reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()), lse.data_ptr<float>(), B, V,
+                          (float)scale, gf.data_ptr<float>(), dx.data_ptr(), cur_stream());
+  return dx;
+}
+
 // ---- GEMM ----------------------------------------------------------------------------------
 // out[M,N] = act(alpha * op(A) op(B) + beta*out + bias).  a_kc: A stored [M,K] (else [K,M]);
 // b_kc: B stored [N,K] (else [K,N]).  Row strides are taken from the 2-D tensors.
@@ -805,6 +830,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
   m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });
+  m.def("softmax_xent_bwd", &softmax_xent_bwd);
   m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"), pybind11::arg("b_kc"),
         pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,

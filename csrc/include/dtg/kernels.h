@@ -88,6 +88,9 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
 // ---- softmax cross-entropy (softmax_xent.hip) ------------------------------------------------
 void softmax_xent(const void* x, int x_bf16, const long long* label, long long B, int V, float scale, float* loss,
                   void* dx, float* lse, hipStream_t st);
+// dx = (softmax(x) - onehot(label)) * scale * (*g) from the forward's lse; g: device scalar (may be null = 1)
+void softmax_xent_bwd(const void* x, int x_bf16, const long long* label, const float* lse, long long B, int V,
+                      float scale, const float* g, void* dx, hipStream_t st);
 
 // ---- GEMM (gemm.hip) -------------------------------------------------------------------------
 // Two-level batch (e.g. [batch, heads] of attention): problem z = zb * nh + zh uses

@@ -189,19 +189,21 @@ class _MLMFn(torch.autograd.Function):
         L.gemm(hm, True, w_t, True, a, 1.0, 0.0, b_t, 2, 0, pre, 1)
         t, _, mean, rstd = L.ln_fwd(a, None, g, b, eps, 0.0, 0, 0.0, 0, False)
         logits = gemm(t, True, word, True, bias=dec_bias)
-        loss_rows, dlogits, _ = L.softmax_xent(logits, labels, 1.0 / denom, True)
+        loss_rows, _, lse = L.softmax_xent(logits, labels, 1.0 / denom, False)
         ctx.mod_params = holder.params
-        ctx.save_for_backward(hm, pre, a, mean, rstd, t, dlogits, w_t, g, word)
+        ctx.scale = 1.0 / denom
+        ctx.save_for_backward(hm, pre, a, mean, rstd, t, logits, labels, lse, w_t, g, word)
         return loss_rows.sum() / denom
 
     @staticmethod
     def backward(ctx, gout):
         L = lib()
-        hm, pre, a, mean, rstd, t, dlogits, w_t, g, word = ctx.saved_tensors
+        hm, pre, a, mean, rstd, t, logits, labels, lse, w_t, g, word = ctx.saved_tensors
         w_t_p, b_t_p, g_p, b_p, word_p, dec_p = ctx.mod_params
         accs = [_gacc(q) for q in ctx.mod_params]
         (gwt, _), (gbt, _), (gg, _), (gb, _), (gword, _), (gdec, _) = accs
-        dl = dlogits * gout.to(dlogits.dtype)
+        # d loss / d logits in one pass from the saved logits + lse, scaled by gout on the device
+        dl = L.softmax_xent_bwd(logits, labels, lse, gout, ctx.scale)
         L.colsum(dl, gdec, True)
         gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
         dt = gemm(dl, True, word, False)                               # [P, H]

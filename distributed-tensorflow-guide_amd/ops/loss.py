@@ -1,8 +1,9 @@
 """Fused softmax cross-entropy (csrc/kernels/softmax_xent.hip).
 
-The forward kernel also emits d(loss)/d(logits) for the requested mean, so backward is a rescale
-by grad_output (a multiply by 1.0 in training).  Rows whose label is < 0 are ignored (loss 0,
-gradient 0) -- the BERT MLM head relies on this.
+The forward kernel computes the per-row loss and logsumexp; the backward kernel produces
+d(loss)/d(logits) in one pass from the saved logits and lse, reading grad_output on the device (no
+host sync and no separate rescale pass).  Rows whose label is < 0 are ignored (loss 0, gradient 0)
+-- the BERT MLM head relies on this.
 """
 import torch
 import torch.nn.functional as F
@@ -13,14 +14,16 @@ from ._native import lib
 class _SoftmaxXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, denom):
-        loss_rows, dlogits, _ = lib().softmax_xent(logits.contiguous(), labels.contiguous(), 1.0 / denom, True)
-        ctx.save_for_backward(dlogits)
+        logits, labels = logits.contiguous(), labels.contiguous()
+        loss_rows, _, lse = lib().softmax_xent(logits, labels, 1.0 / denom, False)
+        ctx.save_for_backward(logits, labels, lse)
+        ctx.scale = 1.0 / denom
         return loss_rows.sum() / denom
 
     @staticmethod
     def backward(ctx, g):
-        (dlogits,) = ctx.saved_tensors
-        return dlogits * g.to(dlogits.dtype), None, None
+        logits, labels, lse = ctx.saved_tensors
+        return lib().softmax_xent_bwd(logits, labels, lse, g, ctx.scale), None, None
 
 
 def softmax_cross_entropy(logits, labels, num_valid=None):
