@@ -17,7 +17,8 @@ all-reduced per image (one model's gradients per step, whatever the batch).  Mea
 - ResNet-50: 10.5k img/s at 128, 12.1k at 256, 12.9k at 384, 13.4k at 512.
 - BERT-base: 6.2k seq/s at 64, 7.6k at 128, 8.2k at 256.
 
-``--batch`` overrides the default.  A timed step is the full training step: forward, fused softmax-xent,
+``--model mnist`` measures BASELINE.json config 2 (MNIST CNN, per-GPU batch 512; a launch-bound step,
+so it replays as one hipGraph by default).  ``--batch`` overrides the default.  A timed step is the full training step: forward, fused softmax-xent,
 backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD apply.  W untimed
 warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
 is the MAX over ranks; rank 0 prints one JSON line.
@@ -48,10 +49,10 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.0)
     ap.add_argument("--model", default="resnet50")
     # whole-step hipGraph replay (parallel/graphs.py; one rank only, multi-rank steps keep their RCCL
-    # all-reduce hooks eager).  Off by default: both steps are GPU-bound (ResNet-50 99.4 % kernel-busy),
-    # so replay measured equal for ResNet-50 (11.93k vs 11.97k img/s) and 2 % slower for BERT
-    # (profiles/r02_baselines)
-    ap.add_argument("--graph", type=int, default=0, help="-1 auto (capture where supported), 0 eager, 1 capture")
+    # all-reduce hooks eager).  auto (-1): on for the launch-bound MNIST step; off for ResNet-50 and
+    # BERT, which are GPU-bound (>= 99 % kernel-busy): replay measured equal for ResNet-50 (11.93k vs
+    # 11.97k img/s) and 2 % slower for BERT (profiles/r02_baselines)
+    ap.add_argument("--graph", type=int, default=-1, help="-1 auto, 0 eager, 1 capture")
     return ap.parse_known_args(argv)[0]
 
 
@@ -79,7 +80,27 @@ def main(argv=None):
     if device.type == "cuda":
         ops.lib()  # fail loudly if the HIP kernels are missing
     dtype = torch.bfloat16
-    if a.model == "bert":
+    if a.model == "mnist":
+        from dtg.models.mnist import MnistCNN, synthetic_mnist
+        a.batch = a.batch or 512
+        model = MnistCNN().to(device)
+        flat = FlatParams(model, compute_dtype=dtype)
+        dp = DataParallel(flat, bucket_mb=a.bucket_mb)
+        dp.broadcast_parameters(0)
+        opt = FusedSGD(flat, lr=(a.lr or 0.01) * world, momentum=0.9)
+        x, y = synthetic_mnist(a.batch, device, dtype, seed=rank)
+        model.train()
+
+        def step():
+            loss = ops.softmax_cross_entropy(model(x), y)
+            loss.backward()
+            dp.finish()
+            opt.step(grad_scale=dp.grad_scale)
+            return loss
+        metric, unit = "images/sec (whole node) MNIST CNN sync DP", "images/sec"
+        conf = {"model": "MNIST CNN (conv5x5-32, conv5x5-64, fc1024, fc10)", "seq_len": None, "image_size": 28,
+                "optimizer": "momentum-sgd (fused)"}
+    elif a.model == "bert":
         from dtg.models import bert
         from dtg.optim import FusedAdam
         a.batch = a.batch or 256
@@ -122,7 +143,8 @@ def main(argv=None):
         conf = {"model": "ResNet-50", "seq_len": None, "image_size": a.image, "optimizer": "momentum-sgd (fused)"}
 
     from dtg.parallel import GraphedStep, capture_supported
-    use_graph = (a.graph == 1 or (a.graph == -1 and capture_supported(world))) and device.type == "cuda"
+    use_graph = (a.graph == 1 or (a.graph == -1 and a.model == "mnist" and capture_supported(world))) \
+        and device.type == "cuda"
     if use_graph:
         # warmup = eager steps on a side stream + the capture; the rest of the warmup replays
         step = GraphedStep(step, warmup=min(2, max(a.warmup - 1, 1)))

@@ -308,7 +308,8 @@ void gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out, double alpha, do
   }
   void* auxp = nullptr;
   if (aux_mode != 0) {
-    TORCH_CHECK(aux_mode == 1 || aux_mode == 2, "aux_mode in {0, 1, 2}");
+    TORCH_CHECK(aux_mode >= 1 && aux_mode <= 4, "aux_mode in {0, 1, 2, 3, 4}");
+    TORCH_CHECK(aux_mode != 3 || act != 0, "aux_mode 3 stores act'(pre): needs an activation");
     TORCH_CHECK(aux.has_value() && aux->defined(), "aux_mode needs an aux tensor");
     TORCH_CHECK(aux->is_cuda() && aux->scalar_type() == at::kBFloat16 && aux->dim() == 2, "aux must be bf16 2-D");
     TORCH_CHECK(aux->size(0) == M && aux->size(1) == N && aux->stride(0) == out.stride(0) && aux->stride(1) == 1,

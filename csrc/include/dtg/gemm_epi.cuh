@@ -13,7 +13,10 @@ struct Epi {
   const float* bias;  // per column (N), may be null
   int act;            // 0 none, 1 relu, 2 gelu(tanh)
   void* aux = nullptr;  // bf16 [M, ldc] side buffer (see aux_mode)
-  int aux_mode = 0;     // 0 none; 1 store the pre-activation to aux; 2 multiply by act'(aux) (act backward)
+  // 0 none; 1 store the pre-activation to aux; 2 multiply by act'(aux) (act backward from the saved
+  // pre-activation); 3 store act'(pre-activation) to aux (forward: the derivative while the
+  // activation's exp is in registers); 4 multiply by aux (act backward from the saved derivative)
+  int aux_mode = 0;
 };
 
 // GELU (tanh form) through its sigmoid identity 0.5 * (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 and
@@ -62,18 +65,21 @@ __device__ __forceinline__ void epi_store8(const Epi& e, int N, int m, int n, fl
     if (e.bias && k < cnt) x += e.bias[n + k];
     v[k] = x;
   }
-  if (e.aux_mode == 1) {
-    if (vec) store8_bf16((bf16_t*)e.aux + off, v);
+  if (e.aux_mode == 1 || e.aux_mode == 3) {
+    float t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = e.aux_mode == 3 ? act_grad(v[k], e.act) : v[k];
+    if (vec) store8_bf16((bf16_t*)e.aux + off, t);
     else
-      for (int k = 0; k < cnt; ++k) ((bf16_t*)e.aux)[off + k] = f2bf(v[k]);
+      for (int k = 0; k < cnt; ++k) ((bf16_t*)e.aux)[off + k] = f2bf(t[k]);
   }
-  if (e.aux_mode == 2) {
+  if (e.aux_mode == 2 || e.aux_mode == 4) {
     float pre[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (vec) load8_bf16((const bf16_t*)e.aux + off, pre);
     else
       for (int k = 0; k < cnt; ++k) pre[k] = bf2f(((const bf16_t*)e.aux)[off + k]);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= act_grad(pre[k], e.act);
+    for (int k = 0; k < 8; ++k) v[k] *= e.aux_mode == 4 ? pre[k] : act_grad(pre[k], e.act);
   } else {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = apply_act(v[k], e.act);
@@ -128,12 +134,33 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
     for (int k = 0; k < 8; ++k) v[k] += b[k];
   }
   if (e.aux_mode == 1) store8_bf16((bf16_t*)e.aux + off, v);
-  if (e.aux_mode == 2) {
+  if (e.aux_mode == 2 || e.aux_mode == 4) {
     float pre[8];
     load8_bf16((const bf16_t*)e.aux + off, pre);
+    if (e.aux_mode == 4) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= act_grad(pre[k], e.act);
+      for (int k = 0; k < 8; ++k) v[k] *= pre[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= act_grad(pre[k], e.act);
+    }
+  } else if (e.aux_mode == 3 && e.act == 2) {  // GELU and its derivative from one sigmoid
+    float d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float x = v[k], sg = gelu_sig(x);
+      const float du = 0.7978845608028654f * fmaf(3.f * 0.044715f * x, x, 1.f);
+      d[k] = fmaf(2.f * x * sg * (1.f - sg), du, sg);
+      v[k] = x * sg;
+    }
+    store8_bf16((bf16_t*)e.aux + off, d);
   } else if (e.act == 1) {
+    if (e.aux_mode == 3) {
+      float d[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = v[k] > 0.f ? 1.f : 0.f;
+      store8_bf16((bf16_t*)e.aux + off, d);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
   } else if (e.act == 2) {

@@ -5,13 +5,14 @@ Per encoder layer (T = batch*seq rows, H hidden, I intermediate; all GEMMs on th
   forward   qkv = x Wqkv^T + b                      (bias in the GEMM epilogue)
             ctx = attention(qkv)                     (2 strided-batched GEMMs + softmax/dropout kernel)
             x1  = LN(x + drop(ctx Wo^T + b))         (LN kernel fuses residual add + dropout)
-            f1  = gelu(x1 W1^T + b1)                 (GELU in the epilogue; pre-activation saved by
-                                                      the same epilogue for backward)
+            f1  = gelu(x1 W1^T + b1)                 (GELU in the epilogue; the same epilogue saves
+                                                      GELU'(pre-activation) for backward, sharing its exp)
             out = LN(x1 + drop(f1 W2^T + b2))
   backward  LN kernels emit both the residual-path gradient and the dropout-masked branch gradient
             (masks regenerated from the counter hash); dgrad GEMMs accumulate the residual gradient
-            (beta = 1) instead of a separate add; GELU' is applied in the dgrad GEMM epilogue from the
-            saved pre-activation; bias gradients are column-sum kernels into the fp32 flat grads;
+            (beta = 1) instead of a separate add; the saved GELU' is applied in the dgrad GEMM epilogue,
+            which also column-sums the result into b1's gradient; the other bias gradients come from the
+            LN backward or column-sum kernels into the fp32 flat grads;
             weight gradients accumulate straight into the flat gradient buffer (grad_sink).
 
 The word embedding is tied to the MLM decoder: the MLM head adds its decoder gradient into the
@@ -71,7 +72,7 @@ class _LayerFn(torch.autograd.Function):
         x1, s1, m1, r1 = L.ln_fwd(ao, x, g1, be1, eps, p_h, s_1, 0.0, 0, True)
         pre = torch.empty(x.shape[0], w_1.shape[0], device=x.device, dtype=x.dtype)
         f1 = torch.empty_like(pre)
-        L.gemm(x1, True, w_1, True, f1, 1.0, 0.0, b_1, 2, 0, pre, 1)
+        L.gemm(x1, True, w_1, True, f1, 1.0, 0.0, b_1, 2, 0, pre, 3)  # pre := gelu'(x1 W1^T + b1)
         f2 = gemm(f1, True, w_2, True, bias=b_2)
         out, s2, m2, r2 = L.ln_fwd(f2, x1, g2, be2, eps, p_h, s_2, 0.0, 0, True)
         ctx.geom = geom
@@ -99,7 +100,7 @@ class _LayerFn(torch.autograd.Function):
         gemm(df2, False, f1, False, out=gw_2, beta=1.0)                       # dW2 += df2^T f1
         dpre = torch.empty_like(pre)
         # df1 * gelu'(pre), and b1's gradient (column sums of it) in the same epilogue
-        L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 2, colsum=gb_1)
+        L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 4, colsum=gb_1)
         gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                      # dW1 += dpre^T x1
         if p_h <= 0:  # df2 aliases ds2: it has been consumed above; accumulate the residual grad into a copy
             ds2 = ds2.clone()

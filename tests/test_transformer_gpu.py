@@ -37,6 +37,17 @@ def test_gemm_gelu_aux_store_and_grad():
     lib().gemm(dy, True, w2, False, d, 1.0, 0.0, None, 2, 0, pre, 2)
     ref = gelu_bwd((dy.float() @ w2.float()), pre.float())
     assert rel(d, ref) < 2e-2
+    # aux_mode 3: the forward stores gelu'(pre) instead of pre; aux_mode 4 multiplies by it
+    dgl = torch.empty_like(out)
+    out3 = torch.empty_like(out)
+    lib().gemm(a, True, w, True, out3, 1.0, 0.0, bias, 2, 0, dgl, 3)
+    assert torch.equal(out3, out)
+    x = ref_pre.clone().requires_grad_()
+    F.gelu(x, approximate="tanh").sum().backward()
+    assert rel(dgl, x.grad) < 1e-2
+    d4 = torch.empty_like(d)
+    lib().gemm(dy, True, w2, False, d4, 1.0, 0.0, None, 2, 0, dgl, 4)
+    assert rel(d4, ref) < 2e-2
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 192), (300, 200, 136)])
