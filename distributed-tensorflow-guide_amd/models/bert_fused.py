@@ -27,7 +27,7 @@ import torch
 from ..ops._native import lib
 from ..ops.gemm import gemm, gelu_bwd
 from ..ops import transformer as T
-from ..parallel import grad_sink
+from ..parallel import grad_sink, overlap
 
 
 _ATTN = os.environ.get("DTG_ATTN", "fused")  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax)
@@ -97,17 +97,20 @@ class _LayerFn(torch.autograd.Function):
         dout = dout.contiguous()
         # LN2: ds2 -> x1 (residual path), df2 -> f2 (dropout branch)
         ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True, gb_2)  # + db2 = sum(df2)
-        gemm(df2, False, f1, False, out=gw_2, beta=1.0)                       # dW2 += df2^T f1
+        with overlap.wgrad_scope(df2, f1):  # weight gradients on the side stream (parallel/overlap.py)
+            gemm(df2, False, f1, False, out=gw_2, beta=1.0)                   # dW2 += df2^T f1
         dpre = torch.empty_like(pre)
         # df1 * gelu'(pre), and b1's gradient (column sums of it) in the same epilogue
         L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 4, colsum=gb_1)
-        gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                      # dW1 += dpre^T x1
+        with overlap.wgrad_scope(dpre, x1):
+            gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                  # dW1 += dpre^T x1
         if p_h <= 0:  # df2 aliases ds2: it has been consumed above; accumulate the residual grad into a copy
             ds2 = ds2.clone()
         gemm(dpre, True, w_1, False, out=ds2, beta=1.0)                       # dx1 = dpre W1 + ds2
         # LN1: ds1 -> x (residual), dao -> attention output projection
         ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True, gb_o)  # + dbo = sum(dao)
-        gemm(dao, False, cx, False, out=gw_o, beta=1.0)
+        with overlap.wgrad_scope(dao, cx):
+            gemm(dao, False, cx, False, out=gw_o, beta=1.0)
         dcx = gemm(dao, True, w_o, False)
         if ctx.fused_attn:
             dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a)
@@ -115,7 +118,8 @@ class _LayerFn(torch.autograd.Function):
             dqkv = torch.empty_like(qkv)
             T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
         L.colsum(dqkv, gb_qkv, True)
-        gemm(dqkv, False, x, False, out=gw_qkv, beta=1.0)
+        with overlap.wgrad_scope(dqkv, x):
+            gemm(dqkv, False, x, False, out=gw_qkv, beta=1.0)
         if p_h <= 0:
             ds1 = ds1.clone()
         gemm(dqkv, True, w_qkv, False, out=ds1, beta=1.0)                     # dx = dqkv Wqkv + ds1

@@ -36,7 +36,7 @@ import torch.nn.functional as F
 
 from ..ops._native import lib
 from ..ops.gemm import gemm
-from ..parallel import grad_sink
+from ..parallel import grad_sink, overlap
 
 
 def _rows(t):
@@ -208,7 +208,8 @@ class _BottleneckFn(torch.autograd.Function):
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
-        gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
+        with overlap.wgrad_scope(dy3, a2):
+            gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
         # BN2 + conv2 (3x3)
         if _FUSE:
             dy2 = L.bn_bwd_part(dp2, y2, q2, b2.weight, m2, i2, False, g[id(b2.weight)], g[id(b2.bias)])[0]
@@ -221,7 +222,8 @@ class _BottleneckFn(torch.autograd.Function):
             dp1 = dp1.view(-1, width)
         else:
             da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
-        L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
+        with overlap.wgrad_scope(dy2_4, a1):
+            L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
         # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
         if _FUSE:
             dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
@@ -240,18 +242,21 @@ class _BottleneckFn(torch.autograd.Function):
                                         g[id(bd.bias)])
             if st == 1:
                 dx2 = gemm(dyd, True, _mat(wd), False)
-                gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
+                with overlap.wgrad_scope(dyd, x2):
+                    gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
             elif lk_in is not None:  # projection dgrad first, so the conv1 dgrad GEMM is the last writer
                 dx2 = L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0).view(-1, c)
-                L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
-                             st, 0)
+                with overlap.wgrad_scope(dyd, x2):
+                    L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
+                                 st, 0)
             else:
                 dx2 = gemm(dy1, True, _mat(w1), False)
                 L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0, out=dx2.view(n, h, w, c),
                              beta=1.0)
                 dx_done = True
-                L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
-                             st, 0)
+                with overlap.wgrad_scope(dyd, x2):
+                    L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
+                                 st, 0)
         else:
             dx2 = dres
         if not dx_done:
@@ -265,7 +270,8 @@ class _BottleneckFn(torch.autograd.Function):
                 lk_in.part, lk_in.part2, lk_in.dp = part, part2, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
-        gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
+        with overlap.wgrad_scope(dy1, x2):
+            gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
         grads = []
         for p, (a, direct) in zip(params, accs):
             if direct:

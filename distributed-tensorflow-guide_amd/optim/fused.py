@@ -27,6 +27,8 @@ class _FlatOptimizer:
         return self.weight_decay if g.name in self.wd_groups else 0.0
 
     def step(self, grad_scale=1.0, zero_grad=True):
+        from ..parallel import overlap
+        overlap.join()  # side-stream weight gradients done before the apply reads them
         self.step_count += 1
         self.hyper[1].add_(1.0)
         for g in self.flat:

@@ -5,3 +5,4 @@ from . import comm  # noqa: F401
 from .async_ps import AsyncPSServer, AsyncPSWorker  # noqa: F401
 from .strategy import MirroredStrategy  # noqa: F401
 from .graphs import GraphedStep, capture_supported  # noqa: F401
+from . import overlap  # noqa: F401

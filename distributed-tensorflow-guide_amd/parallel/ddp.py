@@ -20,7 +20,7 @@ Design:
 import torch
 import torch.distributed as dist
 
-from . import grad_sink
+from . import grad_sink, overlap
 
 
 class _Bucket:
@@ -81,7 +81,14 @@ class DataParallel:
         self._done = set()
 
     def _launch(self, b):
-        b.work = dist.all_reduce(b.view(), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        v = b.view()
+        side = overlap.pending_stream(v)
+        if side is not None:
+            # weight gradients of this bucket may still be running on a side stream (parallel/overlap.py;
+            # single-rank only by default): the main stream waits for them (an event, no host sync) and the
+            # collective is enqueued from the main stream exactly as without the side stream
+            torch.cuda.current_stream(v.device).wait_stream(side)
+        b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _on_direct(self, p):
         if p in self._param_bucket:
@@ -107,6 +114,7 @@ class DataParallel:
 
     def finish(self):
         """Wait for every bucket's all-reduce (launching any that did not fire)."""
+        overlap.join()  # (normally already joined at the end of backward)
         if self.world == 1:
             return
         for b in self.buckets:

@@ -1,0 +1,107 @@
+"""Weight gradients on a second HIP stream, overlapped with the rest of backward.
+
+In a layer's backward the data gradient (dgrad) continues the chain to the layer below, while the
+weight gradient (wgrad) is a leaf: it reads the layer's output gradient and saved input and writes
+the flat gradient buffer, which nothing reads until the all-reduce / optimizer.  dtg's MFMA kernels
+are latency-bound at these sizes (25-36 % MFMA busy, profiles/r02_pmc), so running each wgrad on a
+side stream next to the next layer's BN-backward and dgrad kernels fills the chip with two
+independent kernels instead of one.
+
+    with overlap.wgrad_scope(dy, x):       # inside an autograd backward
+        gemm(dy, False, x, False, out=p.grad, beta=1.0)
+
+* the side stream first waits for everything the main stream has queued (dy is ready);
+* every tensor the side stream reads is ``record_stream``-ed, so the caching allocator does not hand
+  its memory to a main-stream allocation before the side kernels are done;
+* the first scope of a backward pass queues an autograd end-of-backward callback that makes the main
+  stream wait for the side stream, so any consumer after ``backward()`` (optimizer, tests, eager
+  reads of ``.grad``) sees finished gradients;
+* a gradient all-reduce launched during backward (parallel/ddp.py) first makes the main stream wait
+  for the side stream (an event, no host sync), then is enqueued from the main stream as usual.
+
+Single-process only: with more than one rank the weight gradients stay on the main stream.  The
+two-rank rehearsal on one card (gloo, both ranks on cuda:0) ran 9-40x slower with the side stream
+than without it (profiles/r02_overlap), whichever stream enqueued the collectives.  A likely cause is
+the extra stream oversubscribing the per-process hardware queues (4 per process on the box) next to
+the collective library's own streams.  The one-GPU-per-rank RCCL case cannot be measured here, so
+the multi-rank path keeps round 1's validated stream pattern.
+
+``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).
+"""
+import contextlib
+import os
+
+import torch
+
+_ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
+_side = {}      # device index -> side stream
+_main = {}      # device index -> the main stream of the backward the side work belongs to
+_pending = set()
+
+
+def _multi_rank():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def enabled():
+    return _ON and not _multi_rank()
+
+
+def set_enabled(on):
+    global _ON
+    _ON = bool(on)
+
+
+def side_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = _side[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def _join(idx):
+    if idx in _pending:
+        _main[idx].wait_stream(_side[idx])
+        _pending.discard(idx)
+
+
+@contextlib.contextmanager
+def wgrad_scope(*tensors):
+    """Run the enclosed kernel launches on the device's side stream (see module docstring)."""
+    t0 = tensors[0] if tensors else None
+    if t0 is None or not t0.is_cuda or not enabled():
+        yield
+        return
+    idx = t0.device.index
+    main = torch.cuda.current_stream(t0.device)
+    side = side_stream(t0.device)
+    side.wait_stream(main)
+    if idx not in _pending:
+        _pending.add(idx)
+        _main[idx] = main
+        try:  # join at the end of this backward pass
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
+        except RuntimeError:  # not inside a backward pass: the caller joins (join())
+            pass
+    with torch.cuda.stream(side):
+        yield
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(side)
+
+
+def pending_stream(t):
+    """The side stream if it has queued work on t's device this backward pass, else None."""
+    if not t.is_cuda:
+        return None
+    idx = t.device.index
+    return _side[idx] if idx in _pending else None
+
+
+def join(device=None):
+    """Make the main stream wait for all queued side-stream work (no-op when there is none)."""
+    for idx in list(_pending):
+        if device is None or torch.device(device).index in (None, idx):
+            _join(idx)
