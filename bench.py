@@ -154,15 +154,27 @@ def main(argv=None):
     sync()
     comm.barrier()
     sync()
+    diag = os.environ.get("DTG_BENCH_DIAG") == "1"  # per-step times (synchronised: diagnosis only)
+    if device.type == "cuda":
+        torch.cuda.reset_peak_memory_stats(device)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
+        if diag:
+            sync()
+            print(f"step {time.perf_counter() - t0:.4f}", file=sys.stderr, flush=True)
     sync()
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
     dt = comm.all_reduce_max(dt, device)
     final_loss = float(loss.float().item())
+    if device.type == "cuda":  # allocator health (a cudaMalloc retry inside the timed loop synchronises it)
+        ms = torch.cuda.memory_stats(device)
+        print(f"rank {rank} memory: peak reserved {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "
+              f"peak allocated {ms.get('allocated_bytes.all.peak', 0) / 2**30:.1f} GiB, "
+              f"alloc retries {ms.get('num_alloc_retries', 0)}, device mallocs {ms.get('num_device_alloc', 0)}",
+              file=sys.stderr, flush=True)
     gb = a.batch * world
     ips = gb * a.steps / dt
     if rank == 0:

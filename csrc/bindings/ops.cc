@@ -408,16 +408,19 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
 
 // 8-channel input conv (the stem): x [N,H,W,8] NHWC, w [K, Kp] with Kp = ceil64(R*S*8), (r,s,c) columns.
 // with_stats: also the forward BN statistics of y (returned partials, else an empty tensor).
+// stride_w (0 = stride): a separate W stride -- the stem's pixel-pair form is a stride (2, 1) conv.
 std::tuple<Tensor, Tensor> conv_fwd_c8(Tensor x, Tensor w, int64_t R, int64_t S, int64_t stride, int64_t pad,
-                                       bool with_stats) {
+                                       bool with_stats, int64_t stride_w) {
   check_nhwc(x, "x");
   CHECK_IN(w);
   CHECK_DT(w, at::kBFloat16);
+  const int sw = stride_w > 0 ? (int)stride_w : (int)stride;
   const int N = x.size(0), H = x.size(1), W = x.size(2), K = w.size(0);
   TORCH_CHECK(x.size(3) == 8, "conv_fwd_c8 needs 8 input channels");
   TORCH_CHECK(w.dim() == 2 && w.size(1) == (R * S * 8 + 63) / 64 * 64, "w must be [K, ceil64(R*S*8)]");
   TORCH_CHECK(K % 64 == 0, "K % 64");
-  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(stride > 0 && sw > 0 && pad >= 0, "bad stride / pad");
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / sw + 1;
   TORCH_CHECK(P > 0 && Q > 0 && (long long)N * P * Q * K < (1LL << 31), "bad geometry");
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
@@ -430,7 +433,7 @@ std::tuple<Tensor, Tensor> conv_fwd_c8(Tensor x, Tensor w, int64_t R, int64_t S,
   } else {
     part = at::empty({0}, x.options().dtype(at::kFloat));
   }
-  dtg::conv_fwd_c8(cbfp(x), cbfp(w), bfp(y), N, H, W, K, (int)R, (int)S, (int)stride, (int)pad, cur_stream(), bn);
+  dtg::conv_fwd_c8(cbfp(x), cbfp(w), bfp(y), N, H, W, K, (int)R, (int)S, (int)stride, (int)pad, cur_stream(), bn, sw);
   return {y, part};
 }
 
@@ -759,7 +762,7 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp,
 }
 
 // dw (+)= wgrad; dw is [K, R, S, C] contiguous, fp32 or bf16 (beta = 1 accumulates into a flat grad)
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad) {
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad, int64_t stride_w) {
   check_nhwc(dy, "dy");
   check_nhwc(x, "x");
   CHECK_CUDA(dw);
@@ -769,13 +772,14 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
   const int K = dw.size(0), R = dw.size(1), S = dw.size(2);
   TORCH_CHECK(dw.size(3) == C && dy.size(3) == K && dy.size(0) == N, "wgrad shape mismatch");
   TORCH_CHECK(dtg::conv_supported(C, K, R, S, stride, pad, 2), "wgrad shape not supported by the HIP kernel");
-  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / stride + 1;
+  const int sw = stride_w > 0 ? (int)stride_w : (int)stride;
+  const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / sw + 1;
   TORCH_CHECK(dy.size(1) == P && dy.size(2) == Q, "wgrad geometry mismatch");
   c10::DeviceGuard dg(x.device());
-  const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad);
+  const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad, sw);
   auto ws = at::empty({(long long)split * K * R * S * C}, x.options().dtype(at::kFloat));
   dtg::conv_wgrad(cbfp(dy), cbfp(x), dw.data_ptr(), dw.scalar_type() == at::kBFloat16, (float)beta,
-                  ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream());
+                  ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw);
 }
 
 }  // namespace
@@ -789,7 +793,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad", &conv_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"), pybind11::arg("W"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("beta") = 0.0);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"),
+        pybind11::arg("beta"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stride_w") = 0);
   m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
@@ -811,7 +816,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("gamma2"), pybind11::arg("beta2"), pybind11::arg("rmean2"), pybind11::arg("rvar2"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("bits") = pybind11::none());
   m.def("conv_fwd_c8", &conv_fwd_c8, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("R"), pybind11::arg("S"),
-        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("with_stats") = false);
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("with_stats") = false,
+        pybind11::arg("stride_w") = 0);
   m.def("bn_fwd_part", &bn_fwd_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("res"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("bits") = pybind11::none());

@@ -186,10 +186,11 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
                int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi(),
                const bf16_t* wT = nullptr);
 void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
-                 int pad, hipStream_t st, const BnEpi& bn = BnEpi());
+                 int pad, hipStream_t st, const BnEpi& bn = BnEpi(), int stride_w = 0);
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad
-int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad);
+// stride_w (0 = stride): the W stride where it differs from the H stride (C8 forward and wgrad only)
+int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w = 0);
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
-                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st);
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w = 0);
 
 }  // namespace dtg

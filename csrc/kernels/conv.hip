@@ -26,16 +26,20 @@
 namespace dtg {
 using namespace gemm;
 
+// stride applies to both spatial dims except in the C8 forward and the wgrad, which also take a separate
+// W stride (sw): the ResNet stem runs as a stride (2, 1) conv over pixel pairs (stem_pairs in
+// models/resnet_fused.py)
 struct ConvGeom {
-  int N, H, W, C, K, R, S, P, Q, stride, pad;
+  int N, H, W, C, K, R, S, P, Q, stride, pad, sw;
   FastDiv fPQ, fQ, fHW, fW, fC, fS, fK;
 };
 
-static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int sw = 0) {
   ConvGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.stride = stride; g.pad = pad;
+  g.sw = sw > 0 ? sw : stride;
   g.P = (H + 2 * pad - R) / stride + 1;
-  g.Q = (W + 2 * pad - S) / stride + 1;
+  g.Q = (W + 2 * pad - S) / g.sw + 1;
   g.fPQ = FastDiv(g.P * g.Q); g.fQ = FastDiv(g.Q); g.fHW = FastDiv(H * W); g.fW = FastDiv(W);
   g.fC = FastDiv(C); g.fS = FastDiv(S); g.fK = FastDiv(K);
   return g;
@@ -66,7 +70,7 @@ struct FwdA {
       G.fQ.divmod(pq, p, q);
       nbase[i] = (int)n * G.H;
       ih0[i] = (int)p * G.stride - G.pad;
-      iw0[i] = (int)q * G.stride - G.pad;
+      iw0[i] = (int)q * G.sw - G.pad;
     }
   }
   __device__ __forceinline__ void operator()(lds_char* tile, int k0, int wave) const {
@@ -197,7 +201,7 @@ struct WgradB {
       uint32_t n, pq, p, q;
       g->fPQ.divmod((uint32_t)(m < M ? m : 0), n, pq);
       g->fQ.divmod(pq, p, q);
-      const int ih = (int)p * g->stride + dr[i], iw = (int)q * g->stride + ds[i];
+      const int ih = (int)p * g->stride + dr[i], iw = (int)q * g->sw + ds[i];
       const bool ok = m < M && (unsigned)ih < (unsigned)g->H && (unsigned)iw < (unsigned)g->W;
       const void* src = sel(ok, x + ((long long)((int)n * g->H + (ok ? ih : 0)) * g->W + (ok ? iw : 0)) * g->C + cc[i]);
       __builtin_amdgcn_global_load_lds(src, (lds_void*)(tile + kr0 * ROWS * 2), 16, 0, 0);
@@ -482,8 +486,8 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
 
 // 8-channel input (the stem, zero padded 3 -> 8); w is [K][Kp], Kp = ceil64(R*S*8), (r, s, c) order
 void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
-                 int pad, hipStream_t st, const BnEpi& bn) {
-  ConvGeom G = make_geom(N, H, W, 8, K, R, S, stride, pad);
+                 int pad, hipStream_t st, const BnEpi& bn, int stride_w) {
+  ConvGeom G = make_geom(N, H, W, 8, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
   auto run = [&](auto cf) {
@@ -590,8 +594,8 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
   return 1;
 }
 
-int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
-  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   const long long tiles = K <= 64 ? (long long)((No + 255) / 256) : (long long)((K + 127) / 128) * ((No + 127) / 128);
   // target workgroups (DTG_WGRAD_BLOCKS, default 1024 = 4 single-stage workgroups per CU; measured 3-5 %
@@ -604,8 +608,8 @@ int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride
 }
 
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
-                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st) {
-  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w) {
+  ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   int kps = (M + split - 1) / split;
   kps = (kps + BK - 1) / BK * BK;

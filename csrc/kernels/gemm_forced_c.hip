@@ -22,6 +22,10 @@ bool gemm_launch_forced_c(int cfg, int a_kc, int b_kc, const bf16_t* A, long lon
     DTG_CFG_CASE(25, Cfg<128, 128, 1, 4, 64, true>)
     DTG_CFG_CASE(26, Cfg<64, 256, 1, 4, 64, true>)
     DTG_CFG_CASE(27, Cfg<256, 64, 1, 4, 64, true>)
+    DTG_CFG_CASE(28, Cfg<256, 128, 1, 8>)
+    DTG_CFG_CASE(29, Cfg<128, 256, 1, 8>)
+    DTG_CFG_CASE(30, Cfg<256, 128, 1, 8, 64, true>)
+    DTG_CFG_CASE(31, Cfg<128, 256, 1, 8, 64, true>)
     default: return false;
   }
 #undef DTG_CFG_CASE

@@ -34,6 +34,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..ops import conv as conv_ops
 from ..ops._native import lib
 from ..ops.gemm import gemm
 from ..parallel import grad_sink, overlap
@@ -317,11 +318,17 @@ class _StemFn(torch.autograd.Function):
         conv, bn = stem.conv, stem.bn
         k, _, r, s = w.shape
         st, pad = conv.stride, conv.padding
-        x8 = F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous()   # [N, H, W, 8]
-        w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
-        kp = (r * s * 8 + 63) // 64 * 64
-        w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()           # [K, Kp], (r, s, c) columns
-        y4, part = L.conv_fwd_c8(x8, w8, r, s, st, pad, True)      # + BN statistics in the epilogue
+        if conv_ops.stem_pairs_ok(x, w, st):  # 4 channels x 2 pixels per 16-B chunk (ops/conv.py stem_pairs)
+            x8, w8, (rk, sk) = conv_ops.stem_pairs(x, w, st, pad)
+            y4, part = L.conv_fwd_c8(x8, w8, rk, sk, st, 0, True, stride_w=1)  # + BN statistics in the epilogue
+            ctx.pairs = True
+        else:
+            ctx.pairs = False
+            x8 = F.pad(x.permute(0, 2, 3, 1), (0, 8 - c)).contiguous()   # [N, H, W, 8]
+            w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
+            kp = (r * s * 8 + 63) // 64 * 64
+            w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()           # [K, Kp], (r, s, c) columns
+            y4, part = L.conv_fwd_c8(x8, w8, r, s, st, pad, True)      # + BN statistics in the epilogue
         out, idx, smean, sinv = L.stem_bn_pool_fwd(y4, part, gamma, beta, bn.running_mean, bn.running_var,
                                                    bn.momentum, bn.eps, *_POOL)
         ctx.save_for_backward(x8, y4, idx, smean, sinv)
@@ -339,9 +346,14 @@ class _StemFn(torch.autograd.Function):
         (dg, dg_direct), (db, db_direct) = _gacc(gamma), _gacc(beta)
         do4 = dout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
         dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db)[0]
-        dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
-        L.conv_wgrad(dy4, x8, dw8, 0.0, st, pad)
-        dw = dw8[..., :c].permute(0, 3, 1, 2)                      # [K, C, R, S] view
+        if ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
+            dwp = torch.zeros(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)
+            L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1)
+            dw = conv_ops.stem_pairs_dw(dwp, c, s)
+        else:
+            dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
+            L.conv_wgrad(dy4, x8, dw8, 0.0, st, pad)
+            dw = dw8[..., :c].permute(0, 3, 1, 2)                      # [K, C, R, S] view
         grads = []
         if grad_sink.enabled(w):
             w.grad.add_(dw.to(w.grad.dtype))

@@ -10,7 +10,10 @@ Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
     (``conv2d_bias_act``)
   * <= 8 input channels with K % 64 == 0 (the 7x7/2 Cin=3 stem) -> implicit-GEMM conv on the input
     zero-padded to 8 channels (one pixel = one 16-B chunk, csrc/kernels/conv.hip ``conv_fwd_c8``) and
-    the same kernel's wgrad; no dgrad (the stem's input is the image)
+    the same kernel's wgrad; no dgrad (the stem's input is the image).  With <= 4 channels and stride 2
+    the input is instead packed as pixel PAIRS (``stem_pairs``): 4 channels x 2 adjacent pixels per
+    16-B chunk, so the 7x7 filter's K dimension is 7 x 4 x 8 = 224 (padded to 256) instead of
+    7 x 7 x 8 = 392 (padded to 448) -- 43 % fewer MFMA operations and half the input bytes
   * everything else -> MIOpen through torch
 Weight gradients are accumulated straight into the flat gradient buffer (see parallel/grad_sink).
 """
@@ -107,6 +110,40 @@ class _ConvImplicit(torch.autograd.Function):
         return dx, dw4.permute(0, 3, 1, 2), None, None
 
 
+def stem_pairs(x, w, stride, pad):
+    """Pixel-pair form of a stride-2 conv over <= 4 input channels (the ResNet stem).
+
+    Input column iw = 2q - pad + s of output column q lands, in a copy of x padded by `pad` on every side
+    and to 4 channels, at padded column 2q + s: the 16-B pair chunk u = q + s // 2, half s % 2.  So the
+    conv is a (stride 2, stride_w 1, pad 0) conv over [N, Hp, Wp/2, 8] "pixels" (two real pixels x 4
+    channels each) with an R x ceil(S/2) filter whose 8 channels are (s % 2, c).
+
+    Returns (xp [N, Hp, Wp/2, 8], wp [K, ceil64(R*S2*8)], (R, S2)) for conv_fwd_c8/conv_wgrad with
+    stride=stride, pad=0, stride_w=1.  x: NCHW-shaped (channels_last preferred), w: [K, C, R, S].
+    """
+    n, c, h, wd = x.shape
+    k, _, r, s = w.shape
+    s2 = (s + 1) // 2
+    q = (wd + 2 * pad - s) // stride + 1
+    wp = max(wd + 2 * pad, 2 * (q - 1) + 2 * s2)
+    wp += wp & 1
+    xp = F.pad(_nhwc(x), (0, 4 - c, pad, wp - wd - pad, pad, pad)).contiguous()   # [N, Hp, Wp, 4]
+    xp = xp.view(n, h + 2 * pad, wp // 2, 8)
+    w4 = F.pad(w.permute(0, 2, 3, 1), (0, 4 - c, 0, 2 * s2 - s)).reshape(k, r * s2 * 8)  # (r, s//2, s%2, c)
+    kp = (r * s2 * 8 + 63) // 64 * 64
+    return xp, F.pad(w4, (0, kp - r * s2 * 8)).contiguous(), (r, s2)
+
+
+def stem_pairs_ok(x, w, stride):
+    return x.shape[1] <= 4 and stride == 2 and os.environ.get("DTG_STEM_PAIRS", "1") != "0"
+
+
+def stem_pairs_dw(dwp, c, s):
+    """[K, R, S2, 8] pair-form weight gradient -> [K, C, R, S] (a view)."""
+    k, r, s2, _ = dwp.shape
+    return dwp.view(k, r, s2 * 2, 4)[:, :, :s, :c].permute(0, 3, 1, 2)
+
+
 class _ConvC8(torch.autograd.Function):
     """Few-channel input conv (ResNet stem): input padded to 8 channels, weights to [K, ceil64(R*S*8)]."""
 
@@ -114,13 +151,18 @@ class _ConvC8(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad):
         n, c, h, wd = x.shape
         k, _, r, s = w.shape
-        x8 = F.pad(_nhwc(x), (0, 8 - c)).contiguous()          # [N, H, W, 8]
-        w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
-        kp = (r * s * 8 + 63) // 64 * 64
-        w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()       # [K, Kp], (r, s, c) columns
-        y4, _ = lib().conv_fwd_c8(x8, w8, r, s, stride, pad)
+        if stem_pairs_ok(x, w, stride):
+            x8, w8, (rk, sk) = stem_pairs(x, w, stride, pad)
+            y4, _ = lib().conv_fwd_c8(x8, w8, rk, sk, stride, 0, stride_w=1)
+            ctx.geom = (c, k, r, s, stride, pad, True)
+        else:
+            x8 = F.pad(_nhwc(x), (0, 8 - c)).contiguous()          # [N, H, W, 8]
+            w8 = F.pad(w.permute(0, 2, 3, 1), (0, 8 - c)).reshape(k, r * s * 8)
+            kp = (r * s * 8 + 63) // 64 * 64
+            w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()       # [K, Kp], (r, s, c) columns
+            y4, _ = lib().conv_fwd_c8(x8, w8, r, s, stride, pad)
+            ctx.geom = (c, k, r, s, stride, pad, False)
         ctx.save_for_backward(x8)
-        ctx.geom = (c, k, r, s, stride, pad)
         ctx.param = w if grad_sink.enabled(w) else None
         ctx.needs_dx = ctx.needs_input_grad[0]
         return y4.permute(0, 3, 1, 2)
@@ -128,12 +170,17 @@ class _ConvC8(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (x8,) = ctx.saved_tensors
-        c, k, r, s, st, pad = ctx.geom
+        c, k, r, s, st, pad, pairs = ctx.geom
         if ctx.needs_dx:
             raise NotImplementedError("input gradient of the 8-channel stem conv (the image needs none)")
-        dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
-        lib().conv_wgrad(_nhwc(dy).contiguous(), x8, dw8, 0.0, st, pad)
-        dw = dw8[..., :c].permute(0, 3, 1, 2)                    # [K, C, R, S] view
+        if pairs:
+            dwp = torch.zeros(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)
+            lib().conv_wgrad(_nhwc(dy).contiguous(), x8, dwp, 0.0, st, 0, stride_w=1)
+            dw = stem_pairs_dw(dwp, c, s)
+        else:
+            dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
+            lib().conv_wgrad(_nhwc(dy).contiguous(), x8, dw8, 0.0, st, pad)
+            dw = dw8[..., :c].permute(0, 3, 1, 2)                    # [K, C, R, S] view
         p = ctx.param
         if p is not None:
             p.grad.add_(dw.to(p.grad.dtype))

@@ -87,10 +87,13 @@ def test_conv_dgrad_strided_accumulate(R, st, pad, H):
     assert _rel(fresh, ref) < 1e-2
 
 
-@pytest.mark.parametrize("N,C,K,H,R,st,pad", [(2, 3, 64, 32, 7, 2, 3), (2, 3, 64, 23, 7, 2, 3), (3, 4, 128, 16, 3, 1, 1)])
-def test_conv_c8_stem(N, C, K, H, R, st, pad):
-    """Few-channel input (the ResNet stem): input padded to 8 channels, implicit-GEMM fwd + wgrad."""
-    from dtg.ops.conv import _ConvC8
+@pytest.mark.parametrize("pairs", ["1", "0"])
+@pytest.mark.parametrize("N,C,K,H,R,st,pad", [(2, 3, 64, 32, 7, 2, 3), (2, 3, 64, 23, 7, 2, 3), (3, 4, 128, 16, 3, 1, 1),
+                                              (2, 3, 64, 224, 7, 2, 3), (2, 2, 64, 31, 5, 2, 2)])
+def test_conv_c8_stem(N, C, K, H, R, st, pad, pairs, monkeypatch):
+    """Few-channel input (the ResNet stem): implicit-GEMM fwd + wgrad on the input padded to 8 channels,
+    or (stride 2, <= 4 channels, pairs=1) packed as pixel pairs (ops/conv.py stem_pairs)."""
+    monkeypatch.setenv("DTG_STEM_PAIRS", pairs)
     g = torch.Generator(device="cpu").manual_seed(7 + H)
     x = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(K, C, R, R, generator=g) * (2.0 / (C * R * R)) ** 0.5).to(DEV, torch.bfloat16)

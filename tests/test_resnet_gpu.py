@@ -128,14 +128,49 @@ def test_resnet50_step_matches_reference_direction():
     assert torch.isfinite(g.float()).all().item() and g.float().abs().sum().item() > 0
 
 
+def test_wgrad_side_stream_matches_main_stream(monkeypatch):
+    """parallel/overlap.py: weight gradients on the side stream (opt-in) give the same gradients as on the
+    main stream, and backward() returns with them finished (the end-of-backward join)."""
+    from dtg.models.resnet import Bottleneck
+    from dtg.models import resnet_fused
+    from dtg.parallel import overlap
+    monkeypatch.setattr(resnet_fused, "_FUSE", True)
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(2)
+    x0 = torch.randn(8, 64, 16, 16, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy, grads = None, []
+    try:
+        for side in (False, True):
+            overlap.set_enabled(side)
+            torch.manual_seed(0)
+            bl = torch.nn.Sequential(Bottleneck(64, 64, 1), Bottleneck(256, 64, 1), Bottleneck(256, 128, 2))
+            bl = bl.to(dev).to(memory_format=torch.channels_last)
+            bl.train()
+            FlatParams(bl)
+            x = x0.clone().requires_grad_()
+            y = bl(x)
+            if gy is None:
+                gy = torch.randn(y.shape, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            y.backward(gy)
+            assert not overlap._pending  # joined by the end-of-backward callback
+            grads.append([x.grad.float()] + [p.grad.float().clone() for p in bl.parameters()])
+    finally:
+        overlap.set_enabled(False)
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    errs = [rel(ga, gb) for ga, gb in zip(grads[1], grads[0])]
+    assert max(errs) < 1e-2, errs
+
+
+@pytest.mark.parametrize("pairs", ["1", "0"])
 @pytest.mark.parametrize("flat", [False, True])
-def test_fused_stem_matches_unfused(flat, monkeypatch):
+def test_fused_stem_matches_unfused(flat, pairs, monkeypatch):
     """conv7x7/2 -> BN -> ReLU -> maxpool3x3/2 as one node (csrc/kernels/stem.hip: BN statistics from the
     conv epilogue, BN+ReLU+pool in one pass, gather-form backward) equals the op-by-op path: output,
     running statistics and the conv / gamma / beta gradients."""
     from dtg.models.layers import ConvBN
     from dtg.models import resnet_fused
     from dtg.ops.pool import max_pool2d
+    monkeypatch.setenv("DTG_STEM_PAIRS", pairs)  # pixel-pair (ops/conv.py stem_pairs) or 8-channel stem conv
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1)
     x = torch.randn(4, 3, 64, 64, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)

@@ -5,6 +5,7 @@ Warmup dispatches (MIOpen find, first-touch allocations) are dropped by keeping 
 after the (skip+1)-th softmax-xent launch (one per training step), so the table is per timed step.
 
     python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv [--skip 4] [--top 40] [--out f.md]
+    python tools/prof_summary.py gpurun_out/prof/run_results.db          (rocprofv3's default output)
 """
 import argparse
 import collections
@@ -26,6 +27,16 @@ def short(name):
     return name[:48]
 
 
+def load(path):
+    """Kernel rows from a rocprofv3 kernel-trace CSV or its default rocpd SQLite output (.db)."""
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+    con = sqlite3.connect(path)
+    return [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+            for n, s, e in con.execute("select name, start, end from kernels")]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -33,8 +44,8 @@ def main():
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "softmax_xent" in r["Kernel_Name"]]
+    rows = sorted(load(a.trace), key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "softmax_xent_kernel" in r["Kernel_Name"]]  # forward: one per step
     if len(marks) <= a.skip + 1:
         raise SystemExit(f"only {len(marks)} steps in the trace")
     lo, hi = marks[a.skip], marks[-1]
