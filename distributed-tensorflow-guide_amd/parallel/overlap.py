@@ -3,16 +3,18 @@
 In a layer's backward the data gradient (dgrad) continues the chain to the layer below, while the
 weight gradient (wgrad) is a leaf: it reads the layer's output gradient and saved input and writes
 the flat gradient buffer, which nothing reads until the all-reduce / optimizer.  dtg's MFMA kernels
-are latency-bound at these sizes (25-36 % MFMA busy, profiles/r02_pmc), so running each wgrad on a
-side stream next to the next layer's BN-backward and dgrad kernels fills the chip with two
+run at 25-45 % of the dense MFMA peak at these sizes (profiles/r02_gemm, r02_pmc), so running each
+wgrad on a side stream next to the next layer's BN-backward and dgrad kernels fills the chip with two
 independent kernels instead of one.
 
     with overlap.wgrad_scope(dy, x):       # inside an autograd backward
         gemm(dy, False, x, False, out=p.grad, beta=1.0)
 
 * the side stream first waits for everything the main stream has queued (dy is ready);
-* every tensor the side stream reads is ``record_stream``-ed, so the caching allocator does not hand
-  its memory to a main-stream allocation before the side kernels are done;
+* every tensor the side stream reads is kept referenced until the join below, so the caching allocator
+  cannot hand its memory to a main-stream allocation before the side kernels are done.  (This avoids
+  ``record_stream``, which grew the allocator's reserve from 31 to 191 GiB over 25 ResNet-50 b512 steps:
+  every recorded block waits for an event before it is reused, so new blocks keep being allocated);
 * the first scope of a backward pass queues an autograd end-of-backward callback that makes the main
   stream wait for the side stream, so any consumer after ``backward()`` (optimizer, tests, eager
   reads of ``.grad``) sees finished gradients;
@@ -26,7 +28,10 @@ the extra stream oversubscribing the per-process hardware queues (4 per process 
 the collective library's own streams.  The one-GPU-per-rank RCCL case cannot be measured here, so
 the multi-rank path keeps round 1's validated stream pattern.
 
-``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).
+``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).  Measured gain on one rank:
+ResNet-50 +2.3 %, BERT-base +1.1 %.  The record_stream version once ran a whole bench 5x slower
+(191 ms/step instead of 37 ms, same losses), most likely because its allocator reserve kept growing
+(profiles/r02_overlap).
 """
 import contextlib
 import os
@@ -37,6 +42,7 @@ _ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
 _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()
+_keep = {}      # device index -> tensors the side stream reads, released at the join
 
 
 def _multi_rank():
@@ -65,6 +71,8 @@ def _join(idx):
     if idx in _pending:
         _main[idx].wait_stream(_side[idx])
         _pending.discard(idx)
+        # every later main-stream use of these blocks is ordered after the side stream's work
+        _keep.pop(idx, None)
 
 
 @contextlib.contextmanager
@@ -85,11 +93,9 @@ def wgrad_scope(*tensors):
             torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
         except RuntimeError:  # not inside a backward pass: the caller joins (join())
             pass
+    _keep.setdefault(idx, []).extend(t for t in tensors if t is not None)
     with torch.cuda.stream(side):
         yield
-    for t in tensors:
-        if t is not None and t.is_cuda:
-            t.record_stream(side)
 
 
 def pending_stream(t):
