@@ -21,7 +21,26 @@
 namespace dtg {
 namespace gemm {
 
-template <class C, int MODE, class ROWMAP>
+struct RowId {  // identity row map (dense GEMMs)
+  __device__ __forceinline__ int operator()(int m) const { return m; }
+};
+
+// pass height of the prefetching backward epilogue: the tallest of 128 / 64 / 32 rows whose fp32 staging
+// fits the tile's LDS with at most 4 prefetched 8-column groups per thread
+template <class C>
+constexpr int bn_pf_rows() {
+  for (int r = 128; r >= 32; r /= 2)
+    if (r <= C::BM && C::BM % r == 0 && r * (C::BN + 4) * 4 <= C::LDS_BYTES && (r * (C::BN / 8)) % C::NTH == 0 &&
+        r * (C::BN / 8) / C::NTH <= 4)
+      return r;
+  return 32;
+}
+
+// PF: the backward modes prefetch their per-element inputs (epilogue_staged_pf).  That pays where the
+// epilogue's streaming dominates (short reductions, wide outputs: -6 to -11 % on ResNet's 1x1 dgrads) and
+// costs where the extra prefetch registers lower the occupancy of a long main loop (+4 to +28 % on the 3x3
+// dgrads), so the launcher chooses (gemm_bn_dispatch; profiles/r02_epi_pf).
+template <class C, int MODE, class ROWMAP, bool PF = false>
 __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                             const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
   // 4 = mode 3 + a second BN (x2); 5 = not a BN: the GEMM's own bias/activation/aux epilogue
@@ -55,60 +74,123 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       }
     }
   }
-  epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
-    const int row = rowmap(m);
-    if constexpr (MODE == 5) {
-      epi_store8_fast_act(e, row, n, v);
+  if constexpr (MODE == 1 || MODE == 5) {
+    epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
+      const int row = rowmap(m);
+      if constexpr (MODE == 5) {
+        epi_store8_fast_act(e, row, n, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s[k] += bf2f(f2bf(v[k]));  // sum of what was stored
-    } else if constexpr (MODE == 1) {
-      epi_store8_fast(e, row, n, v);
+        for (int k = 0; k < 8; ++k) s[k] += bf2f(f2bf(v[k]));  // sum of what was stored
+      } else {
+        epi_store8_fast(e, row, n, v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float r = bf2f(f2bf(v[k]));  // statistics of what the apply pass will read
-        s[k] += r;
-        q[k] += r * r;
+        for (int k = 0; k < 8; ++k) {
+          const float r = bf2f(f2bf(v[k]));  // statistics of what the apply pass will read
+          s[k] += r;
+          q[k] += r * r;
+        }
       }
-    } else if constexpr (MODE == 2) {
+    });
+  } else if constexpr (!PF) {
+    epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
+      const int row = rowmap(m);
       const long long off = (long long)row * e.ldc + n;
       float xv[8];
       load8_bf16(bn.x + off, xv);
+      if constexpr (MODE == 2) {  // the relu mask is recomputed from x
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
-        v[k] = d;
-        s[k] += d;
-        q[k] += d * xv[k];
-      }
-      store8_bf16((bf16_t*)e.C + off, v);
-    } else {
-      const long long off = (long long)row * e.ldc + n;
-      float xv[8], mk[8], old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      load8_bf16(bn.x + off, xv);
-      if (bn.maskbits) {
-        const uint32_t byte = bn.maskbits[(long long)row * (N >> 3) + (n >> 3)];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) mk[k] = (float)((byte >> k) & 1u);
+        for (int k = 0; k < 8; ++k) {
+          const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
+          v[k] = d;
+          s[k] += d;
+          q[k] += d * xv[k];
+        }
       } else {
-        load8_bf16(bn.mask + off, mk);
-      }
-      if (e.beta != 0.f) load8_bf16((const bf16_t*)e.C + off, old);
+        float mk[8], old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (bn.maskbits) {
+          const uint32_t byte = bn.maskbits[(long long)row * (N >> 3) + (n >> 3)];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
-        v[k] = d;
-        s[k] += d;
-        q[k] += d * xv[k];
-      }
-      if constexpr (two) {
-        float x2v[8];
-        load8_bf16(bn.x2 + off, x2v);
+          for (int k = 0; k < 8; ++k) mk[k] = (float)((byte >> k) & 1u);
+        } else {
+          load8_bf16(bn.mask + off, mk);
+        }
+        if (e.beta != 0.f) load8_bf16((const bf16_t*)e.C + off, old);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) q2[k] += v[k] * x2v[k];
+        for (int k = 0; k < 8; ++k) {
+          const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
+          v[k] = d;
+          s[k] += d;
+          q[k] += d * xv[k];
+        }
+        if constexpr (two) {
+          float x2v[8];
+          load8_bf16(bn.x2 + off, x2v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q2[k] += v[k] * x2v[k];
+        }
       }
       store8_bf16((bf16_t*)e.C + off, v);
-    }
-  });
+    });
+  } else {
+    // backward modes read x (+ mask, residual gradient, x2) per element: prefetched a pass ahead of the
+    // accumulator staging (epilogue_staged_pf), held as raw 16-B vectors until the group is finished
+    constexpr int R = bn_pf_rows<C>();
+    constexpr int GPT = R * CPR / C::NTH;
+    uint4 px[GPT], po[GPT], px2[GPT];
+    uint32_t pm[GPT];
+    const bool has_old = MODE != 2 && e.beta != 0.f;
+    const bool bits = MODE != 2 && bn.maskbits != nullptr;
+    auto pre = [&](int j, int m, int n, bool ok) {
+      if (!ok) return;
+      const int row = rowmap(m);
+      const long long off = (long long)row * e.ldc + n;
+      px[j] = *reinterpret_cast<const uint4*>(bn.x + off);
+      if constexpr (MODE != 2) {
+        if (bits) pm[j] = bn.maskbits[(long long)row * (N >> 3) + (n >> 3)];
+        if (has_old) po[j] = *reinterpret_cast<const uint4*>((const bf16_t*)e.C + off);
+        if constexpr (two) px2[j] = *reinterpret_cast<const uint4*>(bn.x2 + off);
+      }
+    };
+    auto op = [&](int j, int m, int n, float (&v)[8]) {
+      const int row = rowmap(m);
+      const long long off = (long long)row * e.ldc + n;
+      float xv[8];
+      unpack8_bf16(px[j], xv);
+      if constexpr (MODE == 2) {  // the relu mask is recomputed from x
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = fmaf(xv[k], sc[k], sf[k]) > 0.f ? v[k] * e.alpha : 0.f;
+          v[k] = d;
+          s[k] += d;
+          q[k] += d * xv[k];
+        }
+      } else {
+        float mk[8], old[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (bits) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) mk[k] = (float)((pm[j] >> k) & 1u);
+        } else {
+          load8_bf16(bn.mask + off, mk);
+        }
+        if (has_old) unpack8_bf16(po[j], old);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
+          v[k] = d;
+          s[k] += d;
+          q[k] += d * xv[k];
+        }
+        if constexpr (two) {
+          float x2v[8];
+          unpack8_bf16(px2[j], x2v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q2[k] += v[k] * x2v[k];
+        }
+      }
+      store8_bf16((bf16_t*)e.C + off, v);
+    };
+    epilogue_staged_pf<C, R>(smem, acc, bm0, bn0, M, N, pre, op);
+  }
   // epilogue_staged ended with a barrier: the LDS ring is free for the column reduction
   lds_float* red = reinterpret_cast<lds_float*>(smem);
   const int r = tid / CPR;

@@ -11,7 +11,7 @@
 namespace dtg {
 using namespace gemm;
 
-template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false>
+template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false, bool BNPF = false>
 __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
                                                      BnEpi bn) {
@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
   if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
-    epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, N, e, bn, t, [](int m) { return m; });
+    epilogue_bn<CF, BNMODE, RowId, BNPF>(smem, acc, bm0, bn0, M, N, e, bn, t, RowId());
     return;
   }
   if (split_k > 1) {

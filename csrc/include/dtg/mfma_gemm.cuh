@@ -416,5 +416,75 @@ __device__ __forceinline__ void epilogue_staged(lds_char* smem, f32x4 (&acc)[4][
   }
 }
 
+// epilogue_staged with operand prefetch, for epilogues that READ per-element inputs (the BN backward
+// modes: the BN input x, the relu mask, the residual gradient).  Each pass first has every thread issue
+// the loads of all its GPT groups (PRE(j, m, n, ok) -> the caller's registers), then stages the
+// accumulators through LDS and finishes the groups (OP(j, m, n, v)).  The loads of a pass are thus in
+// flight together and under the staging, instead of one group's loads per memory round trip: the
+// stores of group j may alias the next group's loads (same C array), so the compiler cannot hoist
+// them itself.  The barriers are raw s_barrier (LDS counter only): __syncthreads() would also drain
+// the prefetch.  R rows per pass (a multiple of 16 dividing BM); GPT = R*BN/8/NTH groups per thread.
+template <class C, int R, class PRE, class OP>
+__device__ __forceinline__ void epilogue_staged_pf(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+                                                   const PRE& pre, const OP& op) {
+  constexpr int LD = C::BN + 4;
+  constexpr int CPR = C::BN / 8;
+  static_assert(R % 16 == 0 && C::BM % R == 0, "pass height");
+  static_assert(R * LD * 4 <= C::LDS_BYTES, "epilogue staging does not fit");
+  static_assert((R * CPR) % C::NTH == 0, "whole groups per thread");
+  constexpr int GPT = R * CPR / C::NTH;
+  lds_float* st = reinterpret_cast<lds_float*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  __syncthreads();  // operand ring no longer read by anyone
+#pragma unroll
+  for (int pass = 0; pass < C::BM / R; ++pass) {
+    const int prow0 = pass * R;
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+      const int idx = tid + j * C::NTH, rr = idx / CPR, cg = idx % CPR;
+      const int m = bm0 + prow0 + rr, n = bn0 + cg * 8;
+      pre(j, m, n, m < M && n < N);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rblk = wm * 64 + i * 16 - prow0;  // this i-block's row offset inside the pass
+      if (rblk >= 0 && rblk < R) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            st[(rblk + (lane >> 4) * 4 + r) * LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+      const int idx = tid + j * C::NTH, rr = idx / CPR, cg = idx % CPR;
+      const int m = bm0 + prow0 + rr, n = bn0 + cg * 8;
+      if (m < M && n < N) {
+        float v[8];
+        const lds_float* sp = st + rr * LD + cg * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = sp[k];
+        op(j, m, n, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS reads done before the next pass overwrites
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+// unpack 8 bf16 held as one 16-byte vector
+__device__ __forceinline__ void unpack8_bf16(const uint4& v, float (&o)[8]) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  o[4] = __uint_as_float(v.z << 16); o[5] = __uint_as_float(v.z & 0xffff0000u);
+  o[6] = __uint_as_float(v.w << 16); o[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
 }  // namespace gemm
 }  // namespace dtg

@@ -282,7 +282,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 }
 
 // ---- BN-statistics epilogue (gemm_bf16_bn) ---------------------------------------------------------
-template <class CF, int MODE, bool GUARD>
+template <class CF, int MODE, bool GUARD, bool PF>
 static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                       const Epi& e, const BnEpi& bn, hipStream_t st) {
   using SA = DenseKC<GUARD>;
@@ -290,16 +290,29 @@ static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long
   SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE>), dim3(tiles_m * tiles_n, 1, 1), dim3(CF::NTH), 0,
+  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF>), dim3(tiles_m * tiles_n, 1, 1),
+                     dim3(CF::NTH), 0,
                      st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
 }
+
+// DTG_BN_PF: 0 never prefetch, 2 always, default 1 = the shape rule in launch_bn_cfg
+static const int g_bn_pf = getenv("DTG_BN_PF") ? atoi(getenv("DTG_BN_PF")) : 1;
 
 template <class CF, int MODE>
 static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                           const Epi& e, const BnEpi& bn, hipStream_t st) {
   const bool full = (M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0);
-  if (full) launch_bn<CF, MODE, false>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else launch_bn<CF, MODE, true>(A, lda, B, ldb, M, N, K, e, bn, st);
+  // prefetching backward epilogue where the epilogue's streaming dominates: wide outputs or short
+  // reductions (measured per shape, profiles/r02_epi_pf; see epilogue_bn)
+  if constexpr (MODE >= 2 && MODE <= 4) {
+    if (g_bn_pf != 0 && (g_bn_pf == 2 || N >= 512 || K <= 128)) {
+      if (full) launch_bn<CF, MODE, false, true>(A, lda, B, ldb, M, N, K, e, bn, st);
+      else launch_bn<CF, MODE, true, true>(A, lda, B, ldb, M, N, K, e, bn, st);
+      return;
+    }
+  }
+  if (full) launch_bn<CF, MODE, false, false>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else launch_bn<CF, MODE, true, false>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
 template <int MODE>

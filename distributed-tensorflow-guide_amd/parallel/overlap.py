@@ -28,7 +28,8 @@ the extra stream oversubscribing the per-process hardware queues (4 per process 
 the collective library's own streams.  The one-GPU-per-rank RCCL case cannot be measured here, so
 the multi-rank path keeps round 1's validated stream pattern.
 
-``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).  Measured gain on one rank:
+``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs); ``=2`` uses the side stream with
+several ranks too.  Measured gain on one rank:
 ResNet-50 +2.3 %, BERT-base +1.1 %.  The record_stream version once ran a whole bench 5x slower
 (191 ms/step instead of 37 ms, same losses), most likely because its allocator reserve kept growing
 (profiles/r02_overlap).
@@ -39,6 +40,7 @@ import os
 import torch
 
 _ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
+_MULTI = os.environ.get("DTG_WGRAD_STREAM") == "2"  # also with several ranks (rehearsals)
 _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()
@@ -51,7 +53,7 @@ def _multi_rank():
 
 
 def enabled():
-    return _ON and not _multi_rank()
+    return _ON and (_MULTI or not _multi_rank())
 
 
 def set_enabled(on):
