@@ -11,8 +11,11 @@
 // Backward (grid: [B*nh], 8 waves; a wave owns 16 keys; S in {64, 128}):
 //   recomputes P^T = exp(K Q^T * scale + mask - LSE) per 32-query chunk, then
 //   dV += dropout(P)^T dO,  dP^T = V dO^T,  dS^T = P^T (dropout'(dP^T) - D),  dK += dS^T Q * scale;
-//   dS^T is kept whole in LDS, so after one barrier dQ = dS K * scale is a plain MFMA pass per
+//   dS is kept whole in LDS, so after one barrier dQ = dS K * scale is a plain MFMA pass per
 //   16-query wave (no atomics).  D = rowsum(dO * O) is computed in the prologue.
+//   A lane's accumulator elements are 4 consecutive keys of one query, so dropout(P) and dS are
+//   stored query-major (one 8-byte LDS store per matrix and 16-query block) and read back as
+//   transposed fragments (ds_read_b64_tr_b16) where the key-major operand is needed.
 //
 // Fragment conventions as in dtg/mfma_gemm.cuh: mfma(a = X_A[m][k], b = X_B[n][k]) accumulates
 // C[m][n], lane l holding C[(l>>4)*4 + r][l & 15].
@@ -49,9 +52,13 @@ __device__ __forceinline__ v8bf gfrag(const bf16_t* base, long long ld, int row0
 // byte offset of element (row, k) in a [rows][64] bf16 KC tile with the frag_kc swizzle
 __device__ __forceinline__ int kc_off(int row, int k) { return row * 128 + ((((k >> 3) ^ (row & 7))) << 4) + (k & 7) * 2; }
 
-// byte offset of element (k, col) in a [k][32] bf16 MC tile with the frag_mc<32> swizzle
-__device__ __forceinline__ int mc32_off(int k, int col) {
-  return k * 64 + ((((col >> 3) ^ mc_swz<4>(k))) << 4) + (col & 7) * 2;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2v;
+// 4 bf16 (8 bytes) into LDS
+__device__ __forceinline__ void st4_bf16(lds_char* p, const float (&v)[4]) {
+  u32x2v w;
+  w.x = pack_bf2(v[0], v[1]);
+  w.y = pack_bf2(v[2], v[3]);
+  *reinterpret_cast<__attribute__((address_space(3))) u32x2v*>(p) = w;
 }
 
 __device__ __forceinline__ void st_bf16(lds_char* base, int off, float v) {
@@ -198,19 +205,14 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
 // ---------------------------------------------------------------------------------------------
 // Backward, S in {64, 128}: one workgroup (8 waves) per (b, h); wave w owns keys [16w, 16w+16).
 // LDS (S = 128: 74 KB, so two workgroups share a CU): Q and dO as MC tiles (ds_read_b64_tr_b16
-// B-operands), the whole dS^T [S keys][S q] bf16 (written by the key-waves, read back transposed for
-// dQ = dS K -- no atomics), D / LSE / mask rows, and per-wave [16 keys][32 q] scratch for
-// dropout(P)^T.  K is only read by phase 2, so it is staged into the Q tile after phase 1 (its DMA
+// B-operands), the whole dS [S q][S keys] bf16 (written by the key-waves; dK reads it transposed, dQ
+// = dS K row-wise -- no atomics), D / LSE / mask rows, and per-wave [32 q][16 keys] scratch for
+// dropout(P).  K is only read by phase 2, so it is staged into the Q tile after phase 1 (its DMA
 // overlaps the dK / dV stores, which stage through the dO tile).
 //   phase 1 (per 32-query chunk): S^T = K Q^T, dP^T = V dO^T (16 MFMA) -> P^T, dropout, dS^T
 //            -> dV += Pd^T dO, dK += dS^T Q (8 MFMA)
 //   phase 2 (after a barrier): wave w computes dQ for query rows [16w, 16w+16) over all keys.
 // Gradients leave through LDS staging as 16-byte row stores.
-template <int S_>
-__device__ __forceinline__ int dst_off(int key, int q) {  // dS^T [key][q], MC-swizzled 2*S_-byte rows
-  return key * (S_ * 2) + ((((q >> 3) ^ mc_swz<S_ / 8>(key))) << 4) + (q & 7) * 2;
-}
-
 // rows [row0, row0+16) x 64 bf16 of a wave's C-layout accumulators -> global (16-B stores) via a
 // 2 KB per-wave LDS staging area
 __device__ __forceinline__ void store_rows16(lds_char* stg, const f32x4 (&v)[4], float scale, bf16_t* g, long long ldg,
@@ -250,11 +252,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
   lds_char* Qt = smem;                         // MC [q][d]; phase 2: K as MC [key][d]
   lds_char* dOt = Qt + S * 128;                // MC [q][d]; phase 2: per-wave output staging
   lds_char* Kt = Qt;
-  lds_char* dST = dOt + S * 128;               // [S][S] bf16
-  lds_float* Ds = reinterpret_cast<lds_float*>(dST + S * S * 2);
+  lds_char* dSq = dOt + S * 128;               // dS [S q][S key] bf16, MC-swizzled rows
+  lds_float* Ds = reinterpret_cast<lds_float*>(dSq + S * S * 2);
   lds_float* Ls = Ds + S;
   lds_float* Ms = Ls + S;
-  lds_char* scr = reinterpret_cast<lds_char*>(Ms + S) + wave * 1024;  // [16 keys][32 q]
+  lds_char* scr = reinterpret_cast<lds_char*>(Ms + S) + wave * 1024;  // [32 q][16 keys]
   {
     DenseMC<false> qs_{Qg, ld, 64, S};
     DenseMC<false> ds_{dOg, (long long)H, 64, S};
@@ -292,6 +294,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < 4; ++j) dk[j] = dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (has_keys) {
+    constexpr float kLog2e = 1.4426950408889634f;
+    // the lane's 4 keys are fixed for the whole pass: their mask terms (base-2 units) live in registers
+    float msl[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) msl[r] = Ms[kb + rbase + r] * kLog2e;
+    const float sl2 = scale * kLog2e;
     const v8bf ka0 = gfrag(Kg, ld, kb, 0, lane), ka1 = gfrag(Kg, ld, kb, 1, lane);
     const v8bf va0 = gfrag(Vg, ld, kb, 0, lane), va1 = gfrag(Vg, ld, kb, 1, lane);
 #pragma unroll 1
@@ -310,29 +318,34 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
         z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va0, db0, z, 0, 0, 0);
         dpt[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va1, db1, z, 0, 0, 0);
       }
+      // lane: one query q, 4 consecutive keys -> one 8-byte store per matrix into q-major tiles
+      // (dropout(P) into the wave's [32 q][16 key] scratch, dS into dS [S q][S key]); both are
+      // read back as transposed (MC) fragments
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        const int qcol = ni * 16 + (lane & 15), q = qc + qcol;
-        const float lq = Ls[q], dq = Ds[q];
+        const int ql = ni * 16 + (lane & 15), q = qc + ql;
+        const float lq = Ls[q] * kLog2e, dq = Ds[q];
+        const uint32_t ib = ((uint32_t)bh * (uint32_t)S + (uint32_t)q) * (uint32_t)S + (uint32_t)(kb + rbase);
+        float pd[4], dsv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int krow = rbase + r, key = kb + krow;
-          const float p = __expf(st[ni][r] * scale + Ms[key] - lq);
-          float pd = p, dp = dpt[ni][r];
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], sl2, msl[r] - lq));
+          float pv = p, dp = dpt[ni][r];
           if (th) {
-            const bool kp = keep_elem(seed, (uint32_t)(((long long)bh * S + q) * S + key), th);
-            pd = kp ? p * dscale : 0.f;
+            const bool kp = keep_elem(seed, ib + r, th);
+            pv = kp ? p * dscale : 0.f;
             dp = kp ? dp * dscale : 0.f;
           }
-          st_bf16(scr, mc32_off(krow, qcol), pd);
-          st_bf16(dST, dst_off<S>(key, q), p * (dp - dq));
+          pd[r] = pv;
+          dsv[r] = p * (dp - dq);
         }
+        st4_bf16(scr + ql * 32 + rbase * 2, pd);
+        const int key0 = kb + rbase;
+        st4_bf16(dSq + q * (S * 2) + ((((key0 >> 3) ^ mc_swz<S / 8>(q))) << 4) + (key0 & 7) * 2, dsv);
       }
       lds_fence();
-      const int key_l = lane & 15, ch = lane >> 4;
-      const v8bf pa = *reinterpret_cast<const lds_v8bf*>(scr + key_l * 64 + ((ch ^ mc_swz<4>(key_l)) << 4));
-      const int key = kb + key_l, qch = (qc >> 3) + ch;
-      const v8bf sa = *reinterpret_cast<const lds_v8bf*>(dST + key * (S * 2) + ((qch ^ mc_swz<S / 8>(key)) << 4));
+      const v8bf pa = frag_mc<16>(scr, 0, 0, lane);        // dropout(P)^T [16 keys][32 q]
+      const v8bf sa = frag_mc<S>(dSq, kb, qc >> 5, lane);   // dS^T [16 keys][32 q]
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         dv[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_mc<64>(dOt + tq * 8192, j * 16, kq, lane), dv[j], 0,
@@ -343,7 +356,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
       lds_fence();  // scratch rewritten by the next chunk
     }
   }
-  __syncthreads();  // dS^T complete; the Q / dO tiles are free
+  __syncthreads();  // dS complete; the Q / dO tiles are free
   {  // K for dQ = dS K into the Q tile: its DMA is in flight while dK / dV are stored
     DenseMC<false> kss{Kg, ld, 64, S};
 #pragma unroll
@@ -362,9 +375,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
     f32x4 dq[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int qa_ = qr + (lane & 15);
 #pragma unroll
     for (int kk = 0; kk < S / 32; ++kk) {
-      const v8bf a = frag_mc<S>(dST, qr, kk, lane);  // X_A[q][key] = dS
+      // X_A[q][key] = dS: row q of the q-major tile, 8 consecutive keys (its MC swizzle undone)
+      const int c = kk * 4 + (lane >> 4);
+      const v8bf a = *reinterpret_cast<const lds_v8bf*>(dSq + qa_ * (S * 2) + ((c ^ mc_swz<S / 8>(qa_)) << 4));
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         dq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, frag_mc<64>(Kt + (kk >> 1) * 8192, j * 16, kk & 1, lane),
