@@ -308,9 +308,16 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
       f32x4 st[2], dpt[2];
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        const v8bf qb0 = gfrag(Qg, ld, qc + ni * 16, 0, lane), qb1 = gfrag(Qg, ld, qc + ni * 16, 1, lane);
-        const v8bf db0 = gfrag(dOg, (long long)H, qc + ni * 16, 0, lane);
-        const v8bf db1 = gfrag(dOg, (long long)H, qc + ni * 16, 1, lane);
+        // B fragments (16 queries x 32 d) read row-wise out of the staged MC tiles (undoing their swizzle)
+        // instead of from global memory
+        const int qrow = (qc & 63) + ni * 16 + (lane & 15), cb = lane >> 4;
+        const int sw = mc_swz<8>(qrow);
+        const lds_char* qt = Qt + tq * 8192 + qrow * 128;
+        const lds_char* dt = dOt + tq * 8192 + qrow * 128;
+        const v8bf qb0 = *reinterpret_cast<const lds_v8bf*>(qt + ((cb ^ sw) << 4));
+        const v8bf qb1 = *reinterpret_cast<const lds_v8bf*>(qt + (((4 + cb) ^ sw) << 4));
+        const v8bf db0 = *reinterpret_cast<const lds_v8bf*>(dt + ((cb ^ sw) << 4));
+        const v8bf db1 = *reinterpret_cast<const lds_v8bf*>(dt + (((4 + cb) ^ sw) << 4));
         f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
         z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka0, qb0, z, 0, 0, 0);
         st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka1, qb1, z, 0, 0, 0);
