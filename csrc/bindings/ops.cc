@@ -380,9 +380,10 @@ static bool dgrad_wt() {
   return on;
 }
 
-// dx (= or +=, beta) dgrad; `out` (optional, [N,H,W,C] bf16) receives it in place
+// dx (= or +=, beta) dgrad; `out` (optional, [N,H,W,C] bf16) receives it in place.  zero_rest=False: a
+// strided dgrad leaves the rows no filter tap reaches unwritten (see gemm_bn's sub2_hw)
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, c10::optional<Tensor> out,
-                  double beta) {
+                  double beta, bool zero_rest) {
   check_nhwc(dy, "dy");
   check_nhwc(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), K = dy.size(3);
@@ -401,8 +402,10 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     dx = at::empty({N, H, W, C}, dy.options());
   }
   Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();  // see conv_dgrad_bn
+  TORCH_CHECK(zero_rest || (stride == 2 && R == 1 && S == 1 && pad == 0 && beta == 0.0),
+              "zero_rest=False is for a stride-2 1x1 dgrad (beta 0)");
   dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, (float)beta, cur_stream(),
-                  dtg::BnEpi(), wT.defined() ? cbfp(wT) : nullptr);
+                  dtg::BnEpi(), wT.defined() ? cbfp(wT) : nullptr, zero_rest ? 1 : 0);
   return dx;
 }
 
@@ -485,7 +488,8 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
                                    c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                                    c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled,
                                    c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
-                                   c10::optional<Tensor> invstd2, c10::optional<Tensor> part2) {
+                                   c10::optional<Tensor> invstd2, c10::optional<Tensor> part2,
+                                   c10::optional<std::tuple<int64_t, int64_t>> sub2_hw) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
@@ -536,6 +540,11 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
         bn.mean2 = mean2->data_ptr<float>();
         bn.invstd2 = invstd2->data_ptr<float>();
         bn.part2 = part2->data_ptr<float>();
+      }
+      if (sub2_hw.has_value()) {  // `out` holds a stride-2 projection dgrad: only its even (h, w) rows are valid
+        const auto [sh, sw] = *sub2_hw;
+        TORCH_CHECK(bt != 0.f && sh > 0 && sw > 0 && (long long)M % (sh * sw) == 0, "sub2_hw needs out and M = N*H*W");
+        dtg::bn_sub2_rows(bn, (int)sh, (int)sw);
       }
       if (mask->scalar_type() == at::kByte) {  // packed bits [M, N/8]
         TORCH_CHECK(mask->numel() == (long long)M * (N / 8), "mask bits shape mismatch");
@@ -792,7 +801,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_dgrad", &conv_dgrad, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"), pybind11::arg("W"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("out") = pybind11::none(),
-        pybind11::arg("beta") = 0.0);
+        pybind11::arg("beta") = 0.0, pybind11::arg("zero_rest") = true);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"),
         pybind11::arg("beta"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stride_w") = 0);
   m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
@@ -801,7 +810,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("beta") = pybind11::none(), pybind11::arg("mask") = pybind11::none(),
         pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false,
         pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none(),
-        pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none());
+        pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none(),
+        pybind11::arg("sub2_hw") = pybind11::none());
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
         pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
   m.def("bn_bwd2_part", &bn_bwd2_part);

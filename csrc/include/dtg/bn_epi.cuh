@@ -21,6 +21,17 @@
 namespace dtg {
 namespace gemm {
 
+// BnEpi::old_sub2: does output row `row` = (n, h, w) carry a residual gradient (h and w even)?
+__device__ __forceinline__ bool bn_row_has_old(const BnEpi& bn, int row) {
+  if (!bn.old_sub2) return true;
+  const uint32_t r = (uint32_t)row;
+  const uint32_t n = (uint32_t)(((uint64_t)__umulhi(r, bn.hw_m) + r) >> bn.hw_l);
+  const uint32_t hw = r - n * bn.old_hw;
+  const uint32_t h = (uint32_t)(((uint64_t)__umulhi(hw, bn.w_m) + hw) >> bn.w_l);
+  const uint32_t w = hw - h * bn.old_w;
+  return ((h | w) & 1u) == 0;
+}
+
 struct RowId {  // identity row map (dense GEMMs)
   __device__ __forceinline__ int operator()(int m) const { return m; }
 };
@@ -114,7 +125,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         } else {
           load8_bf16(bn.mask + off, mk);
         }
-        if (e.beta != 0.f) load8_bf16((const bf16_t*)e.C + off, old);
+        if (e.beta != 0.f && bn_row_has_old(bn, row)) load8_bf16((const bf16_t*)e.C + off, old);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
@@ -138,6 +149,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
     constexpr int GPT = R * CPR / C::NTH;
     uint4 px[GPT], po[GPT], px2[GPT];
     uint32_t pm[GPT];
+    bool ho[GPT];
     const bool has_old = MODE != 2 && e.beta != 0.f;
     const bool bits = MODE != 2 && bn.maskbits != nullptr;
     auto pre = [&](int j, int m, int n, bool ok) {
@@ -147,7 +159,8 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       px[j] = *reinterpret_cast<const uint4*>(bn.x + off);
       if constexpr (MODE != 2) {
         if (bits) pm[j] = bn.maskbits[(long long)row * (N >> 3) + (n >> 3)];
-        if (has_old) po[j] = *reinterpret_cast<const uint4*>((const bf16_t*)e.C + off);
+        ho[j] = has_old && bn_row_has_old(bn, row);
+        if (ho[j]) po[j] = *reinterpret_cast<const uint4*>((const bf16_t*)e.C + off);
         if constexpr (two) px2[j] = *reinterpret_cast<const uint4*>(bn.x2 + off);
       }
     };
@@ -172,7 +185,7 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
         } else {
           load8_bf16(bn.mask + off, mk);
         }
-        if (has_old) unpack8_bf16(po[j], old);
+        if (ho[j]) unpack8_bf16(po[j], old);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;

@@ -50,7 +50,27 @@ struct BnEpi {
   const float* mean2 = nullptr;
   const float* invstd2 = nullptr;
   float* part2 = nullptr;
+  // mode 3/4, optional: the residual gradient (beta * C) exists only on the rows (n, h, w) with h and w
+  // even -- what a stride-2 1x1 projection's dgrad writes; every other row reads as zero and is not
+  // loaded, so the projection's dgrad need not zero-fill them.  Row -> (h, w) by multiply-shift division
+  // (magic m, shift l of H*W and of W, host-computed: bn_sub2_rows).
+  int old_sub2 = 0;
+  uint32_t old_hw = 1, old_w = 1, hw_m = 0, hw_l = 0, w_m = 0, w_l = 0;
 };
+
+// host: fill the old_sub2 fields of a BnEpi for an H x W image
+inline void bn_sub2_rows(BnEpi& bn, int H, int W) {
+  auto magic = [](uint32_t d, uint32_t& m, uint32_t& l) {
+    l = 0;
+    while ((1u << l) < d) ++l;
+    m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+  };
+  bn.old_sub2 = 1;
+  bn.old_hw = (uint32_t)(H * W);
+  bn.old_w = (uint32_t)W;
+  magic(bn.old_hw, bn.hw_m, bn.hw_l);
+  magic(bn.old_w, bn.w_m, bn.w_l);
+}
 
 // ---- batchnorm NHWC (batchnorm.hip) ----------------------------------------------------------
 long long bn_workspace_floats(long long M, int C);
@@ -184,7 +204,7 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
 // wT (optional): the weight transposed to [C][(r,s,k)] (K-contiguous), used by the stride-1 kernels
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
                int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi(),
-               const bf16_t* wT = nullptr);
+               const bf16_t* wT = nullptr, int zero_rest = 1);
 void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
                  int pad, hipStream_t st, const BnEpi& bn = BnEpi(), int stride_w = 0);
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad

@@ -507,8 +507,10 @@ static int dgrad_sched(int sc, const ConvGeom& G) {
   return (g_conv_stages[1] <= 0 && G.R * G.S > 1 && sc == 2) ? 3 : sc;
 }
 
+// zero_rest = 0: rows of dx no residue class reaches (a 1x1 stride-2 dgrad: all but the even (h, w)) are
+// left unwritten -- for a consumer that reads only the written rows (BnEpi::old_sub2)
 static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t* w, bf16_t* dx, float beta,
-                              hipStream_t st, const BnEpi& bn) {
+                              hipStream_t st, const BnEpi& bn, int zero_rest) {
   const int s = G.stride;
   bool empty = false;
   for (int ph = 0; ph < s; ++ph)
@@ -517,7 +519,7 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
       if (r0 >= G.R || s0 >= G.S || ph >= G.H || pw >= G.W) empty = true;
     }
   if (empty && bn.mode != 0) return 0;  // rows no launch writes would be missing from the statistics
-  if (empty && beta == 0.f) {  // residue classes no tap reaches are zero
+  if (empty && beta == 0.f && zero_rest) {  // residue classes no tap reaches are zero
     DTG_HIP_CHECK(hipMemsetAsync(dx, 0, (size_t)G.N * G.H * G.W * G.C * sizeof(bf16_t), st));
     beta = 1.f;
   }
@@ -564,9 +566,9 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
 }
 
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
-               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn, const bf16_t* wT) {
+               int stride, int pad, float beta, hipStream_t st, const BnEpi& bn, const bf16_t* wT, int zero_rest) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
-  if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st, bn);
+  if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st, bn, zero_rest);
   const int M = N * H * W;
   Epi e{dx, C, 1, 1.f, beta, nullptr, 0};
   auto run = [&](auto cf) {

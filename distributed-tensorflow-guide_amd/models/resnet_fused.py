@@ -58,6 +58,9 @@ def _krsc(w):  # channels_last [K, C, R, S] -> contiguous [K, R, S, C] view
 
 _FUSE = os.environ.get("DTG_BN_FUSE", "1") != "0"
 _LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction (needs _FUSE)
+# linked stride-2 projection: its dgrad writes only the even (h, w) rows, which the next mode-3 GEMM alone
+# reads (no zero-fill of a [N, H, W, C] gradient per stage transition); 0 restores the zero-filled form
+_SUB2 = os.environ.get("DTG_DGRAD_SUB2", "1") != "0"
 
 
 class _Bn3Link:
@@ -231,6 +234,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         dx_done = False
+        sub2_hw = None
         lk_in = ctx.link_in
         ctx.link_in = None
         if lk_in is not None and lk_in.y3.shape != x2.shape:
@@ -246,7 +250,13 @@ class _BottleneckFn(torch.autograd.Function):
                 with overlap.wgrad_scope(dyd, x2):
                     gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
             elif lk_in is not None:  # projection dgrad first, so the conv1 dgrad GEMM is the last writer
-                dx2 = L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0).view(-1, c)
+                # only the even (h, w) rows of a stride-2 1x1 dgrad are written; the mode-3 GEMM below reads
+                # just those (sub2_hw) instead of a zero-filled full tensor
+                sub2 = st == 2 and _SUB2
+                dx2 = L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0,
+                                   zero_rest=not sub2).view(-1, c)
+                if sub2:
+                    sub2_hw = (h, w)
                 with overlap.wgrad_scope(dyd, x2):
                     L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
                                  st, 0)
@@ -267,7 +277,7 @@ class _BottleneckFn(torch.autograd.Function):
                     part2 = L.bn_part_alloc(dy1, c, pooled=True)
                 _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
                                     mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
-                                    invstd2=lk_in.idd, part2=part2)
+                                    invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw)
                 lk_in.part, lk_in.part2, lk_in.dp = part, part2, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)

@@ -76,7 +76,8 @@ def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, m
         assert torch.allclose(ba, bb, rtol=1e-3, atol=1e-4)
 
 
-def test_bn3_link_chain_matches_unlinked(monkeypatch):
+@pytest.mark.parametrize("sub2", [True, False])
+def test_bn3_link_chain_matches_unlinked(sub2, monkeypatch):
     """Three chained blocks (projection, identity, strided projection).  With the BN3 link each block's
     BN3 statistics are reduced by the NEXT block's last dgrad epilogue (mode 3); without it, by the
     block's own reduction pass.  Both runs share the same forward bit for bit (the link only changes
@@ -86,6 +87,7 @@ def test_bn3_link_chain_matches_unlinked(monkeypatch):
     from dtg.models.resnet import Bottleneck
     from dtg.models import resnet_fused
     monkeypatch.setattr(resnet_fused, "_FUSE", True)
+    monkeypatch.setattr(resnet_fused, "_SUB2", sub2)  # strided projection dgrad: even rows only (no zero fill)
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1)
     x0 = torch.randn(4, 64, 16, 16, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
