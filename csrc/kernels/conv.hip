@@ -604,8 +604,12 @@ int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride
   // faster than 512 on the 14x14 / 28x28 3x3 layers, 256 is 25 % slower); more splits also grow the fp32
   // slabs the reduce pass re-reads
   static const long long target = getenv("DTG_WGRAD_BLOCKS") ? atoll(getenv("DTG_WGRAD_BLOCKS")) : 1024;
+  // up to 1024 splits when the fp32 slabs stay small (<= 64 MB): the stem's single 64 x 224 output tile
+  // needs 1024 splits to reach 1024 workgroups (at 256 it ran 256 workgroups, one per CU)
+  const long long slab = (long long)K * No * 4;
   int s = 1;
-  while (tiles * s < target && (long long)M / (s * 2) >= 1024 && s < 256) s *= 2;
+  while (tiles * s < target && (long long)M / (s * 2) >= 1024 && (s < 256 || (s < 1024 && 2 * s * slab <= (64LL << 20))))
+    s *= 2;
   return s;
 }
 
