@@ -104,6 +104,21 @@ std::vector<Tensor> stem_bn_pool_fwd(Tensor y, Tensor part, Tensor gamma, Tensor
   return {out, idx, smean, sinv};
 }
 
+// x [N,H,W,C] (C <= 4, NHWC view of a channels_last image) -> [N, H+2*pad, Wp/2, 8]: the pixel-pair
+// stem input (ops/conv.py stem_pairs), zero padding and packing in one pass
+Tensor stem_pack_pairs(Tensor x, int64_t pad, int64_t Wp) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(),
+              "x must be a contiguous NHWC bf16 GPU tensor");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C >= 1 && C <= 4 && pad >= 0 && Wp % 2 == 0 && Wp >= W + pad, "bad pair-packing geometry");
+  const int Hp = H + 2 * (int)pad;
+  TORCH_CHECK((long long)N * Hp * Wp * 4 < (1LL << 40), "too large");
+  c10::DeviceGuard dg(x.device());
+  auto xp = at::empty({N, Hp, Wp / 2, 8}, x.options());
+  dtg::stem_pack_pairs(cbfp(x), bfp(xp), N, H, W, C, (int)pad, Hp, (int)Wp, cur_stream());
+  return xp;
+}
+
 // dout [N,P,Q,C], idx, y [N,H,W,C] -> dy [N,H,W,C] (gradient of the stem conv output); dgamma/dbeta
 // accumulated into the given fp32 buffers when both are passed, else returned fresh
 std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor gamma, Tensor beta, Tensor smean,
@@ -176,6 +191,7 @@ void register_pool_ops(pybind11::module_& m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("stem_bn_pool_fwd", &stem_bn_pool_fwd);
+  m.def("stem_pack_pairs", &stem_pack_pairs, pybind11::arg("x"), pybind11::arg("pad"), pybind11::arg("Wp"));
   m.def("stem_bn_pool_bwd", &stem_bn_pool_bwd, pybind11::arg("dout"), pybind11::arg("idx"), pybind11::arg("y"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("smean"), pybind11::arg("sinv"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("pad"), pybind11::arg("dgamma_acc") = pybind11::none(),

@@ -184,6 +184,9 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                       float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
                       int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st);
 long long stem_bwd_workspace_floats(long long M, int C);
+// x [N,H,W,C<=4] -> xp [N, H+2*pad, Wp, 4], zero padded (the pixel-pair stem conv's input)
+void stem_pack_pairs(const bf16_t* x, bf16_t* xp, int N, int H, int W, int C, int pad, int Hp, int Wp,
+                     hipStream_t st);
 void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
                       const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
                       float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st);

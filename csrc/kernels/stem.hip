@@ -17,6 +17,8 @@
 //
 // Tie semantics equal the unfused path: values are rounded to bf16 (what apply would have stored)
 // before the window comparison, and the first maximum in window order wins.
+#include <stdlib.h>
+
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/bn_finalize.cuh"
@@ -34,15 +36,16 @@ __device__ __forceinline__ float bn_relu_bf(float y, float sc, float sf) {
 }
 
 // ---- forward: out[n,p,q,c] = max over the window of bf16(relu(y*scale + shift)), idx = argmax ----
-// KT > 0: the window size as a compile-time constant: the KT*KT loads are unrolled with clamped
-// addresses and a validity flag (all in flight together).  KT = 0: runtime g.k (the one launched).
+// KT > 0: the window size as a compile-time constant: all KT*KT 16-byte loads are issued before the
+// first comparison (clamped addresses + a validity flag) and held as raw bf16 vectors (4 VGPRs each,
+// not 8 floats), so the window's loads are in flight together without the register cost of the
+// earlier unrolled form.  KT = 0: runtime g.k (any window).
 template <int KT>
 __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             bf16_t* __restrict__ out, uint8_t* __restrict__ idx,
                                                             StemGeom g) {
   const unsigned c8n = g.C >> 3;
   const unsigned total = (unsigned)g.N * g.P * g.Q * c8n;  // < 2^31 (host check)
-  const int K = KT > 0 ? KT : g.k;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c8 = (int)(i % c8n);
     unsigned t = i / c8n;
@@ -61,28 +64,45 @@ __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __rest
     }
     const int h0 = p * g.s - g.pad, w0 = q * g.s - g.pad;
     const bf16_t* yn = y + (long long)n * g.H * g.W * g.C + c8 * 8;
+    auto take = [&](const uint4& raw, bool ok, uint8_t wi) {
+      float v[8];
+      gemm::unpack8_bf16(raw, v);
 #pragma unroll
-    for (int r = 0; r < (KT > 0 ? KT : 1); ++r) {
-      for (int rr = (KT > 0 ? r : 0); rr < (KT > 0 ? r + 1 : K); ++rr) {
+      for (int k = 0; k < 8; ++k) {
+        const float a = ok ? bn_relu_bf(v[k], sc[k], sf[k]) : -INFINITY;
+        if (a > m[k]) {  // strict: the first maximum in window order wins ties
+          m[k] = a;
+          am[k] = wi;
+        }
+      }
+    };
+    if constexpr (KT > 0) {
+      uint4 raw[KT * KT];
+      bool okk[KT * KT];
+#pragma unroll
+      for (int rr = 0; rr < KT; ++rr) {
         const int h = h0 + rr;
         const bool hok = (unsigned)h < (unsigned)g.H;
 #pragma unroll
-        for (int c = 0; c < (KT > 0 ? KT : 1); ++c) {
-          for (int cc = (KT > 0 ? c : 0); cc < (KT > 0 ? c + 1 : K); ++cc) {
-            const int w = w0 + cc;
-            const bool ok = hok && (unsigned)w < (unsigned)g.W;
-            float v[8];
-            load8_bf16(yn + ((long long)(hok ? h : 0) * g.W + (ok ? w : 0)) * g.C, v);
-            const uint8_t wi = (uint8_t)(rr * K + cc);
+        for (int cc = 0; cc < KT; ++cc) {
+          const int w = w0 + cc;
+          const bool ok = hok && (unsigned)w < (unsigned)g.W;
+          okk[rr * KT + cc] = ok;
+          raw[rr * KT + cc] =
+              *reinterpret_cast<const uint4*>(yn + ((long long)(hok ? h : 0) * g.W + (ok ? w : 0)) * g.C);
+        }
+      }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const float a = ok ? bn_relu_bf(v[k], sc[k], sf[k]) : -INFINITY;
-              if (a > m[k]) {  // strict: the first maximum in window order wins ties
-                m[k] = a;
-                am[k] = wi;
-              }
-            }
-          }
+      for (int j = 0; j < KT * KT; ++j) take(raw[j], okk[j], (uint8_t)j);
+    } else {
+      for (int rr = 0; rr < g.k; ++rr) {
+        const int h = h0 + rr;
+        const bool hok = (unsigned)h < (unsigned)g.H;
+        for (int cc = 0; cc < g.k; ++cc) {
+          const int w = w0 + cc;
+          const bool ok = hok && (unsigned)w < (unsigned)g.W;
+          const uint4 raw = *reinterpret_cast<const uint4*>(yn + ((long long)(hok ? h : 0) * g.W + (ok ? w : 0)) * g.C);
+          take(raw, ok, (uint8_t)(rr * g.k + cc));
         }
       }
     }
@@ -240,6 +260,44 @@ __global__ void __launch_bounds__(kBlk) stem_bwd_dx_kernel(const bf16_t* __restr
   }
 }
 
+// ---- input packing for the pixel-pair stem conv (ops/conv.py stem_pairs) ---------------------------
+// x [N, H, W, C] (C <= 4, NHWC bf16) -> xp [N, H + 2*pad, Wp, 4] zero-padded (pad rows/columns on the
+// top/left, the rest on the bottom/right, channels C..3 zero): one thread per 16-byte output chunk
+// (two padded pixels), so the padding zeros and the copy are one pass (F.pad: a fill + a strided copy).
+__global__ void __launch_bounds__(256) stem_pack_pairs_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ xp,
+                                                              int N, int H, int W, int C, int pad, int Hp, int Wp2) {
+  const long long total = (long long)N * Hp * Wp2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int u = (int)(i % Wp2);
+    const long long t = i / Wp2;
+    const int hp = (int)(t % Hp);
+    const int n = (int)(t / Hp);
+    const int h = hp - pad;
+    uint32_t w4[4] = {0u, 0u, 0u, 0u};  // 8 bf16: pixel 2u (channels 0..3), pixel 2u + 1
+    if ((unsigned)h < (unsigned)H) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int w = 2 * u + e - pad;
+        if ((unsigned)w < (unsigned)W) {
+          const bf16_t* src = x + (((long long)n * H + h) * W + w) * C;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c < C) w4[e * 2 + (c >> 1)] |= (uint32_t)src[c] << (16 * (c & 1));
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(xp + i * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+  }
+}
+
+void stem_pack_pairs(const bf16_t* x, bf16_t* xp, int N, int H, int W, int C, int pad, int Hp, int Wp,
+                     hipStream_t st) {
+  const long long total = (long long)N * Hp * (Wp / 2);
+  hipLaunchKernelGGL(stem_pack_pairs_kernel, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, xp, N, H, W, C,
+                     pad, Hp, Wp / 2);
+}
+
 static StemGeom stem_geom(int N, int H, int W, int C, int k, int s, int pad, int P, int Q) {
   StemGeom g;
   g.N = N; g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.k = k; g.s = s; g.pad = pad;
@@ -276,9 +334,12 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                                                          sinv, momentum, eps, coef, nullptr, nullptr, 0);
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   const long long total = (long long)N * P * Q * (C / 8);
-  // KT = 0 (runtime window loop): the unrolled KT = 3 instance measured slower (240 vs 163 us at batch 256:
-  // nine 16-B loads in flight per lane cost more occupancy than they buy)
-  hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+  // 3x3 windows (ResNet): the unrolled form with raw-vector loads (DTG_STEM_POOL_KT=0: the runtime loop)
+  static const bool kt3 = !getenv("DTG_STEM_POOL_KT") || atoi(getenv("DTG_STEM_POOL_KT")) != 0;
+  if (k == 3 && kt3)
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+  else
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
 }
 
 void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,

@@ -127,8 +127,11 @@ def stem_pairs(x, w, stride, pad):
     q = (wd + 2 * pad - s) // stride + 1
     wp = max(wd + 2 * pad, 2 * (q - 1) + 2 * s2)
     wp += wp & 1
-    xp = F.pad(_nhwc(x), (0, 4 - c, pad, wp - wd - pad, pad, pad)).contiguous()   # [N, Hp, Wp, 4]
-    xp = xp.view(n, h + 2 * pad, wp // 2, 8)
+    if x.is_cuda and x.dtype == torch.bfloat16:  # one packing pass (csrc/kernels/stem.hip)
+        xp = lib().stem_pack_pairs(_nhwc(x).contiguous(), pad, wp)
+    else:
+        xp = F.pad(_nhwc(x), (0, 4 - c, pad, wp - wd - pad, pad, pad)).contiguous()   # [N, Hp, Wp, 4]
+        xp = xp.view(n, h + 2 * pad, wp // 2, 8)
     w4 = F.pad(w.permute(0, 2, 3, 1), (0, 4 - c, 0, 2 * s2 - s)).reshape(k, r * s2 * 8)  # (r, s//2, s%2, c)
     kp = (r * s2 * 8 + 63) // 64 * 64
     return xp, F.pad(w4, (0, kp - r * s2 * 8)).contiguous(), (r, s2)

@@ -107,3 +107,17 @@ def test_conv_c8_stem(N, C, K, H, R, st, pad, pairs, monkeypatch):
     y.backward(gy)
     yr.backward(gy.float())
     assert _rel(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("N,C,H,W,pad,S", [(2, 3, 224, 224, 3, 7), (3, 3, 23, 29, 3, 7), (2, 2, 31, 31, 2, 5),
+                                           (1, 4, 12, 14, 1, 3), (1, 1, 10, 10, 0, 4)])
+def test_stem_pack_pairs_matches_pad(N, C, H, W, pad, S):
+    """The one-pass pixel-pair packing kernel (stem.hip) equals the F.pad form of ops/conv.py stem_pairs."""
+    from dtg.ops.conv import stem_pairs
+    g = torch.Generator(device="cpu").manual_seed(H + W)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, C, S, S, generator=g).bfloat16()
+    ref, wref, _ = stem_pairs(x, w, 2, pad)          # CPU: F.pad
+    got, wgot, _ = stem_pairs(x.to(DEV), w.to(DEV), 2, pad)
+    assert got.shape == ref.shape and torch.equal(got.cpu(), ref)
+    assert torch.equal(wgot.cpu(), wref)
