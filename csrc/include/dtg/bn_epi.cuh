@@ -51,9 +51,15 @@ constexpr int bn_pf_rows() {
 // epilogue's streaming dominates (short reductions, wide outputs: -6 to -11 % on ResNet's 1x1 dgrads) and
 // costs where the extra prefetch registers lower the occupancy of a long main loop (+4 to +28 % on the 3x3
 // dgrads), so the launcher chooses (gemm_bn_dispatch; profiles/r02_epi_pf).
+// Per-thread column statistics of an epilogue (s: sum, q: raw moment, q2: the second BN's raw moment),
+// carried across the tiles of a multi-tile workgroup (BnEpi::tiles_per_wg) and reduced once.
+struct BnAcc {
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
 template <class C, int MODE, class ROWMAP, bool PF = false>
-__device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
-                                            const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
+__device__ __forceinline__ void epilogue_bn_stream(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+                                                   const Epi& e, const BnEpi& bn, const ROWMAP& rowmap, BnAcc& st) {
   // 4 = mode 3 + a second BN (x2); 5 = not a BN: the GEMM's own bias/activation/aux epilogue
   // (epi_store8_fast_act) plus the column sums of the stored output added into bn.part[N] (fp32) --
   // the bias gradient of the layer whose output gradient this GEMM produces, without a re-read
@@ -66,10 +72,11 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
   // block reduction: sum(d * xhat) = invstd * (sum(d * x) - mean * sum(d)).  Keeping mean/invstd out of
   // the row loop saves 16 VGPRs (32 in mode 4), which is what puts the 128x128 backward epilogues
   // under the 128-VGPR line of 4 workgroups per CU.
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float (&s)[8] = st.s;
+  float (&q)[8] = st.q;
   float sc[8], sf[8];
   // mode 3 with a second BN on the same gradient (x2: the projection shortcut's BN input): sum(dp*x2)
-  float q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float (&q2)[8] = st.q2;
   constexpr bool two = MODE == 4;  // a separate instantiation: mode 3 keeps its register budget
   if constexpr (MODE == 2) {  // the relu mask is recomputed from x: gamma*xhat + beta > 0
     if (n0 < N) {
@@ -204,7 +211,21 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
     };
     epilogue_staged_pf<C, R>(smem, acc, bm0, bn0, M, N, pre, op);
   }
-  // epilogue_staged ended with a barrier: the LDS ring is free for the column reduction
+}
+
+// Block reduction of the BnAcc column statistics + one atomic add per column into the partial slot
+// slot_id % kBnStatSlots (mode 5: straight into bn.part[N]).  The LDS ring must be free (every
+// epilogue_bn_stream ends with a barrier).
+template <class C, int MODE>
+__device__ __forceinline__ void epilogue_bn_reduce(lds_char* smem, int bn0, int N, const BnEpi& bn, int slot_id,
+                                                   const BnAcc& st) {
+  constexpr int CPR = C::BN / 8, RW = C::NTH / CPR;
+  constexpr bool two = MODE == 4;
+  const int tid = threadIdx.x, cg = tid % CPR;
+  const float (&s)[8] = st.s;
+  const float (&q)[8] = st.q;
+  const float (&q2)[8] = st.q2;
+  const int tile_id = slot_id;
   lds_float* red = reinterpret_cast<lds_float*>(smem);
   const int r = tid / CPR;
   if constexpr (MODE == 5) {
@@ -251,6 +272,15 @@ __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], 
       }
     }
   }
+}
+
+// stream + reduce for one tile (the conv kernels; gemm_kernel loops over BnEpi::tiles_per_wg tiles itself)
+template <class C, int MODE, class ROWMAP, bool PF = false>
+__device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
+                                            const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {
+  BnAcc st;
+  epilogue_bn_stream<C, MODE, ROWMAP, PF>(smem, acc, bm0, bn0, M, N, e, bn, rowmap, st);
+  epilogue_bn_reduce<C, MODE>(smem, bn0, N, bn, tile_id, st);
 }
 
 }  // namespace gemm
