@@ -71,6 +71,21 @@ def main(argv=None):
     from dtg.parallel import FlatParams, DataParallel, comm
     from dtg.optim import FusedSGD
     from dtg import ops
+    from dtg.utils import StepTimer, trace_range
+
+    def train_step(forward_loss, dp, opt):
+        """forward -> backward (bucketed all-reduce fired from inside) -> join -> fused apply, with roctx
+        ranges around each phase when DTG_TRACE=1 (dtg.utils.trace)"""
+        def step():
+            with trace_range("dtg.forward"):
+                loss = forward_loss()
+            with trace_range("dtg.backward"):
+                loss.backward()
+            with trace_range("dtg.allreduce.join"):
+                dp.finish()
+            opt.step(grad_scale=dp.grad_scale)
+            return loss
+        return step
 
     rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
     a.bucket_mb = a.bucket_mb or (25.0 if a.model == "bert" else 8.0)
@@ -91,12 +106,7 @@ def main(argv=None):
         x, y = synthetic_mnist(a.batch, device, dtype, seed=rank)
         model.train()
 
-        def step():
-            loss = ops.softmax_cross_entropy(model(x), y)
-            loss.backward()
-            dp.finish()
-            opt.step(grad_scale=dp.grad_scale)
-            return loss
+        step = train_step(lambda: ops.softmax_cross_entropy(model(x), y), dp, opt)
         metric, unit = "images/sec (whole node) MNIST CNN sync DP", "images/sec"
         conf = {"model": "MNIST CNN (conv5x5-32, conv5x5-64, fc1024, fc10)", "seq_len": None, "image_size": 28,
                 "optimizer": "momentum-sgd (fused)"}
@@ -113,12 +123,7 @@ def main(argv=None):
         batch = bert.synthetic_batch(a.batch, a.seq, cfg, device, max_predictions=20, seed=rank)
         model.train()
 
-        def step():
-            loss = model(*batch)
-            loss.backward()
-            dp.finish()
-            opt.step(grad_scale=dp.grad_scale)
-            return loss
+        step = train_step(lambda: model(*batch), dp, opt)
         metric, unit = "sequences/sec (whole node) BERT-base pre-training sync DP", "sequences/sec"
         conf = {"model": "BERT-base (MLM+NSP)", "seq_len": a.seq, "optimizer": "adam-wd (fused)"}
     else:
@@ -132,13 +137,7 @@ def main(argv=None):
         x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
         model.train()
 
-        def step():
-            out = model(x)
-            loss = ops.softmax_cross_entropy(out, y)
-            loss.backward()
-            dp.finish()
-            opt.step(grad_scale=dp.grad_scale)
-            return loss
+        step = train_step(lambda: ops.softmax_cross_entropy(model(x), y), dp, opt)
         metric, unit = METRIC, "images/sec"
         conf = {"model": "ResNet-50", "seq_len": None, "image_size": a.image, "optimizer": "momentum-sgd (fused)"}
 
@@ -154,21 +153,25 @@ def main(argv=None):
     sync()
     comm.barrier()
     sync()
-    diag = os.environ.get("DTG_BENCH_DIAG") == "1"  # per-step times (synchronised: diagnosis only)
+    # per-step GPU times from HIP events (dtg.utils.StepTimer: read back after the loop, no sync inside)
+    diag = StepTimer(batch_size=a.batch, device=device) if os.environ.get("DTG_BENCH_DIAG") == "1" else None
     if device.type == "cuda":
         torch.cuda.reset_peak_memory_stats(device)
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        if diag:
+            diag.start()
         loss = step()
         if diag:
-            sync()
-            print(f"step {time.perf_counter() - t0:.4f}", file=sys.stderr, flush=True)
+            diag.stop()
     sync()
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
     dt = comm.all_reduce_max(dt, device)
     final_loss = float(loss.float().item())
+    if diag:
+        print(f"rank {rank} step times: {diag.times_ms()}  {diag.summary()}", file=sys.stderr, flush=True)
     if device.type == "cuda":  # allocator health (a cudaMalloc retry inside the timed loop synchronises it)
         ms = torch.cuda.memory_stats(device)
         print(f"rank {rank} memory: peak reserved {ms.get('reserved_bytes.all.peak', 0) / 2**30:.1f} GiB, "

@@ -6,6 +6,7 @@ training step can be captured in a hipGraph and replayed with a new schedule val
 import torch
 
 from ..ops import optim_kernels as K
+from ..utils.trace import trace_range
 
 
 class _FlatOptimizer:
@@ -30,9 +31,10 @@ class _FlatOptimizer:
         from ..parallel import overlap
         overlap.join()  # side-stream weight gradients done before the apply reads them
         self.step_count += 1
-        self.hyper[1].add_(1.0)
-        for g in self.flat:
-            self._apply(g, grad_scale, zero_grad)
+        with trace_range("dtg.apply"):  # roctx range (DTG_TRACE=1)
+            self.hyper[1].add_(1.0)
+            for g in self.flat:
+                self._apply(g, grad_scale, zero_grad)
 
     def state_dict(self):
         return {"step": self.step_count, "lr": self.lr,

@@ -52,6 +52,9 @@ def _recv(t, src=None, group=None):
     return peer
 
 
+from ..utils.trace import traced
+
+
 class _HostSend:
     """isend of a host copy; keeps the copy alive until wait()."""
 
@@ -119,6 +122,7 @@ class AsyncPSWorker:
         DOWNPOUR/DOWNPOUR.py:129-135)."""
         self.pull()
 
+    @traced("dtg.ps.pull")
     def pull(self):
         for buf in _group_payload_params(self.flat):
             _recv(buf, src=self.ps, group=self.pg)
@@ -130,6 +134,7 @@ class AsyncPSWorker:
                 if g.mirror is not None:
                     g.master.copy_(g.mirror)
 
+    @traced("dtg.ps.push")
     def step_done(self):
         """Call once per local step after backward.  Pushes/pulls every ``window`` steps; returns
         True when an exchange with the PS happened."""
@@ -199,6 +204,7 @@ class AsyncPSServer:
         self._send_works[w] = [_isend(s, dst=w, group=self.pg) for s in snap]
         self._pulled_version[w] = self.version
 
+    @traced("dtg.ps.apply")
     def _apply(self, w):
         bufs = self._recv[w]
         saved = [g.grad for g in self.flat]

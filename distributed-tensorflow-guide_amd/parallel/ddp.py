@@ -21,6 +21,7 @@ import torch
 import torch.distributed as dist
 
 from . import grad_sink, overlap
+from ..utils.trace import trace_range
 
 
 class _Bucket:
@@ -88,7 +89,8 @@ class DataParallel:
             # single-rank only by default): the main stream waits for them (an event, no host sync) and the
             # collective is enqueued from the main stream exactly as without the side stream
             torch.cuda.current_stream(v.device).wait_stream(side)
-        b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        with trace_range("dtg.allreduce.bucket%d" % b.index):  # roctx range (DTG_TRACE=1)
+            b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     def _on_direct(self, p):
         if p in self._param_bucket:
