@@ -104,10 +104,13 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
     qa[0] = gfrag(Qg, ld, q0, 0, lane);
     qa[1] = gfrag(Qg, ld, q0, 1, lane);
   }
+  // the additive key mask of batch b, staged once (was one global load per 16-key block and chunk,
+  // each on the critical path of the softmax)
+  lds_float* Mk = reinterpret_cast<lds_float*>(smem + 2 * S * 128 + kFwdWaves * 2048);
+  for (int i = threadIdx.x; i < S; i += 64 * kFwdWaves) Mk[i] = mask ? mask[(long long)b * S + i] : 0.f;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (!active) return;  // (no barrier below this point)
-  const float* mk = mask ? mask + (long long)b * S : nullptr;
   float m[4], l[4];
   f32x4 o[4];
 #pragma unroll
@@ -132,7 +135,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
     for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float madd = mk ? mk[kc * 64 + j * 16 + (lane & 15)] : 0.f;
+      const float madd = Mk[kc * 64 + j * 16 + (lane & 15)];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         s[j][r] = s[j][r] * scale + madd;
@@ -158,7 +161,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
         rs[r] += p;
         float pd = p;
         if (th) {
-          const uint32_t idx = (uint32_t)(((long long)bh * S + q0 + rbase + r) * S + key);
+          const uint32_t idx = ((uint32_t)bh * (uint32_t)S + (uint32_t)(q0 + rbase + r)) * (uint32_t)S + (uint32_t)key;
           pd = keep_elem(seed, idx, th) ? p * dscale : 0.f;
         }
         st_bf16(scr, kc_off(rbase + r, j * 16 + (lane & 15)), pd);
@@ -408,7 +411,7 @@ int attn_fused_supported(int S, int dh, int backward) {
   return backward ? (S == 64 || S == 128) : (S <= 512);
 }
 
-static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + kFwdWaves * 2048; }
+static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + kFwdWaves * 2048 + (size_t)S * 4; }
 static size_t bwd_lds(int S) { return (size_t)2 * S * 128 + (size_t)S * S * 2 + 3 * S * 4 + 8 * 1024; }
 
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,

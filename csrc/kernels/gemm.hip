@@ -263,6 +263,14 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
     return;
   }
+  // opt-in (DTG_GEMM_WIDE=1): wide outputs over a short reduction (BERT's FFN1 forward / FFN2 dgrad,
+  // 32768x3072x768) on the 128x256 8-wave single stage.  Plain GEMMs measured 156 vs 165 us (nt) and 163
+  // vs 167 us (nn) in tools/gemm_ab.py (profiles/r02_gemm/gemm_ab_8wave_*.txt), but with the real GELU /
+  // aux epilogues BERT-base b256 ran 8.92k vs 9.05k seq/s (profiles/r02_gemm/bert_wide*.log): off.
+  static const bool wide_on = getenv("DTG_GEMM_WIDE") && atoi(getenv("DTG_GEMM_WIDE")) != 0;
+  if (wide_on && split_k == 1 && bt.count == 1 && N >= 3072 && kps <= 1024 && M >= 8192 &&
+      gemm_launch_forced(29, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt))
+    return;
   // Tile width follows N so the streamed activation operand A is read as few times as possible:
   // 256x64 for N <= 64, 64x256 for N >= 256 with K <= 256, else 128x128 (r01_tiles sweeps).  LDS ring depth: a single stage
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
