@@ -616,8 +616,57 @@ void emb_word_bwd(const bf16_t* ds, const long long* sorted, const long long* pe
   hipLaunchKernelGGL(emb_word_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, st, ds, sorted, perm, gW, T, H);
 }
 
+// Position-embedding grad, batch split: one workgroup per position, G groups of threads each summing
+// every G-th batch row of one 8-column chunk (unrolled by 4: independent loads in flight), then an LDS
+// reduction over the groups.  The one-wave-per-position form ran 128 waves for BERT's 128 positions,
+// each walking its 256 batch rows serially (161 us for 50 MB at batch 256).
+template <int G>
+__global__ void __launch_bounds__(1024) emb_pos_bwd_split_kernel(const bf16_t* __restrict__ ds,
+                                                                 bf16_t* __restrict__ gP, int T, int S, int H) {
+  extern __shared__ float red[];  // [G][nch * 8]
+  const int nch = H >> 3, p = blockIdx.x;
+  const int c = threadIdx.x % nch, g = threadIdx.x / nch;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g < G) {
+    const long long step = (long long)G * S;
+    long long r = p + (long long)g * S;
+    for (; r + 3 * step < T; r += 4 * step) {
+      float t0[8], t1[8], t2[8], t3[8];
+      load8_bf16(ds + r * H + c * 8, t0);
+      load8_bf16(ds + (r + step) * H + c * 8, t1);
+      load8_bf16(ds + (r + 2 * step) * H + c * 8, t2);
+      load8_bf16(ds + (r + 3 * step) * H + c * 8, t3);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += (t0[k] + t1[k]) + (t2[k] + t3[k]);
+    }
+    for (; r < T; r += step) {
+      float t[8];
+      load8_bf16(ds + r * H + c * 8, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += t[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[(g * nch + c) * 8 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nch * 8; i += blockDim.x) {
+    float v = 0.f;
+#pragma unroll
+    for (int j = 0; j < G; ++j) v += red[j * nch * 8 + i];
+    const long long o = (long long)p * H + i;
+    gP[o] = f2bf(bf2f(gP[o]) + v);
+  }
+}
+
 void emb_pos_bwd(const bf16_t* ds, bf16_t* gP, int T, int S, int H, hipStream_t st) {
   if (T <= 0) return;
+  const int nch = H / 8;
+  if (H % 8 == 0 && nch <= 128) {
+    const int threads = nch * 8;  // G = 8 groups
+    hipLaunchKernelGGL(emb_pos_bwd_split_kernel<8>, dim3(S), dim3(threads), (size_t)8 * nch * 8 * sizeof(float), st,
+                       ds, gP, T, S, H);
+    return;
+  }
   hipLaunchKernelGGL(emb_pos_bwd_kernel, dim3(rows_grid(S)), dim3(256), 0, st, ds, gP, T, S, H);
 }
 

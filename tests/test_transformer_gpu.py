@@ -289,3 +289,16 @@ def test_bert_attention_paths_agree(attn, monkeypatch):
     lr.backward()
     for (n, pf), pr in zip(fused.named_parameters(), ref.parameters()):
         assert rel(pf.grad, pr.grad) < 5e-2, n
+
+
+@pytest.mark.parametrize("B,S,H", [(64, 128, 768), (3, 128, 1024), (5, 7, 64), (2, 16, 1032)])
+def test_pos_embedding_grad_accumulates(B, S, H):
+    """emb_pos_bwd (batch-split form for H/8 <= 128, the wave-per-position form above) adds
+    sum over the batch of ds[b*S + p] into an existing bf16 gradient."""
+    torch.manual_seed(B + S)
+    ds = torch.randn(B * S, H, device=dev).bfloat16()
+    g0 = torch.randn(S, H, device=dev).bfloat16()
+    gP = g0.clone()
+    lib().emb_pos_bwd(ds, gP, S)
+    ref = g0.float() + ds.float().view(B, S, H).sum(0)
+    assert rel(gP, ref) < 1e-2
