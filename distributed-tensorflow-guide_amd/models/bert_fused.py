@@ -25,7 +25,7 @@ import os
 import torch
 
 from ..ops._native import lib
-from ..ops.gemm import gemm, gelu_bwd
+from ..ops.gemm import gemm
 from ..ops import transformer as T
 from ..parallel import grad_sink, overlap
 
@@ -191,7 +191,7 @@ class _MLMFn(torch.autograd.Function):
         eps, denom = geom
         pre = torch.empty(hm.shape[0], w_t.shape[0], device=hm.device, dtype=hm.dtype)
         a = torch.empty_like(pre)
-        L.gemm(hm, True, w_t, True, a, 1.0, 0.0, b_t, 2, 0, pre, 1)
+        L.gemm(hm, True, w_t, True, a, 1.0, 0.0, b_t, 2, 0, pre, 3)  # pre := gelu'(hm W^T + b), as in FFN1
         t, _, mean, rstd = L.ln_fwd(a, None, g, b, eps, 0.0, 0, 0.0, 0, False)
         logits = gemm(t, True, word, True, bias=dec_bias)
         loss_rows, _, lse = L.softmax_xent(logits, labels, 1.0 / denom, False)
@@ -213,7 +213,7 @@ class _MLMFn(torch.autograd.Function):
         gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
         dt = gemm(dl, True, word, False)                               # [P, H]
         da, _ = L.ln_bwd(dt, a, g, mean, rstd, gg, gb, 0.0, 0, 0.0, 0, False)
-        dpre = gelu_bwd(da, pre)
+        dpre = torch.mul(da, pre)                                      # pre holds gelu'(pre-activation)
         L.colsum(dpre, gbt, True)
         gemm(dpre, False, hm, False, out=gwt, beta=1.0)
         dhm = gemm(dpre, True, w_t, False)
