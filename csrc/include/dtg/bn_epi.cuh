@@ -52,7 +52,7 @@ constexpr int bn_pf_rows() {
 // costs where the extra prefetch registers lower the occupancy of a long main loop (+4 to +28 % on the 3x3
 // dgrads), so the launcher chooses (gemm_bn_dispatch; profiles/r02_epi_pf).
 // Per-thread column statistics of an epilogue (s: sum, q: raw moment, q2: the second BN's raw moment),
-// carried across the tiles of a multi-tile workgroup (BnEpi::tiles_per_wg) and reduced once.
+// streamed by epilogue_bn_stream and reduced once per workgroup by epilogue_bn_reduce.
 struct BnAcc {
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
@@ -274,7 +274,7 @@ __device__ __forceinline__ void epilogue_bn_reduce(lds_char* smem, int bn0, int 
   }
 }
 
-// stream + reduce for one tile (the conv kernels; gemm_kernel loops over BnEpi::tiles_per_wg tiles itself)
+// stream + reduce for one tile (every BN-epilogue GEMM / conv workgroup owns exactly one output tile)
 template <class C, int MODE, class ROWMAP, bool PF = false>
 __device__ __forceinline__ void epilogue_bn(lds_char* smem, f32x4 (&acc)[4][4], int bm0, int bn0, int M, int N,
                                             const Epi& e, const BnEpi& bn, int tile_id, const ROWMAP& rowmap) {

@@ -39,34 +39,23 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
     t = xcd_remap(blockIdx.x, ntiles);
     split = 0;
   }
-  f32x4 acc[4][4];
-  if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
-    // workgroup t: N tile t % tiles_n, M tiles [(t / tiles_n) * tpw, + tpw) -- statistics summed over them
-    const int tpw = bn.tiles_per_wg, tn = t % tiles_n, tm0 = (t / tiles_n) * tpw;
-    const int tiles_m = (M + CF::BM - 1) / CF::BM;
-    const int bn0 = tn * CF::BN;
-    BnAcc st;
-    for (int i = 0; i < tpw && tm0 + i < tiles_m; ++i) {
-      const int bm0 = (tm0 + i) * CF::BM;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, 0, K, acc);
-      epilogue_bn_stream<CF, BNMODE, RowId, BNPF>(smem, acc, bm0, bn0, M, N, e, bn, RowId(), st);
-    }
-    epilogue_bn_reduce<CF, BNMODE>(smem, bn0, N, bn, t, st);
-    return;
-  }
   const int tm = t / tiles_n, tn = t % tiles_n;
   const int bm0 = tm * CF::BM, bn0 = tn * CF::BN;
   const int kbeg = split * k_per_split;
   const int kend = min(K, kbeg + k_per_split);
+  f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
+  if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
+    // one tile per workgroup, the column statistics live only in the epilogue.  (Several M tiles per
+    // workgroup, statistics carried across their main loops, ran ResNet-50 3-4 % slower: the gemm bn3
+    // kernels 4.8 -> 6.2 ms per step, profiles/r02_bn_tiles and profiles/r02_bn_revert.)
+    epilogue_bn<CF, BNMODE, RowId, BNPF>(smem, acc, bm0, bn0, M, N, e, bn, t, RowId());
+    return;
+  }
   if (split_k > 1) {
     float* slab = ws + (long long)split * M * N;
     const bool vec = (N & 3) == 0;

@@ -56,9 +56,6 @@ struct BnEpi {
   // (magic m, shift l of H*W and of W, host-computed: bn_sub2_rows).
   int old_sub2 = 0;
   uint32_t old_hw = 1, old_w = 1, hw_m = 0, hw_l = 0, w_m = 0, w_l = 0;
-  // dense GEMMs: consecutive M tiles (same N tile) per workgroup; their column statistics are summed in
-  // registers and reduced + added once (1 = one tile per workgroup)
-  int tiles_per_wg = 1;
 };
 
 // host: fill the old_sub2 fields of a BnEpi for an H x W image

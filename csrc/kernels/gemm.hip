@@ -290,13 +290,6 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 }
 
 // ---- BN-statistics epilogue (gemm_bf16_bn) ---------------------------------------------------------
-// target workgroup count of the BN-epilogue GEMMs (DTG_BN_WGS; default 0 = one tile per workgroup).
-// Several M tiles per workgroup (one statistics reduction + atomic per column per workgroup) measured
-// slower: ResNet-50 b512 13.53k img/s with one tile per workgroup, 13.45k at 2048 workgroups, 13.16k at
-// 1024; BERT 9.10k vs 9.01k (profiles/r02_bn_tiles) -- the per-tile atomics are not the bottleneck,
-// and the longer workgroups hide latency worse.
-static const long long g_bn_tpw_target = getenv("DTG_BN_WGS") ? atoll(getenv("DTG_BN_WGS")) : 0;
-
 template <class CF, int MODE, bool GUARD, bool PF>
 static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                       const Epi& e, const BnEpi& bn, hipStream_t st) {
@@ -305,16 +298,8 @@ static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long
   SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  // several M tiles per workgroup on long grids: one statistics reduction + atomic per column per
-  // workgroup instead of per tile (a 1605632 x 256 output has 25088 tiles = 6.4M column atomics)
-  BnEpi b = bn;
-  const long long tiles = (long long)tiles_m * tiles_n;
-  b.tiles_per_wg = g_bn_tpw_target > 0 && tiles > g_bn_tpw_target ? (int)((tiles + g_bn_tpw_target - 1) / g_bn_tpw_target)
-                                                                 : 1;
-  const int wgs_m = (tiles_m + b.tiles_per_wg - 1) / b.tiles_per_wg;
-  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF>), dim3(wgs_m * tiles_n, 1, 1),
-                     dim3(CF::NTH), 0,
-                     st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), b);
+  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF>), dim3(tiles_m * tiles_n, 1, 1),
+                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
 }
 
 // DTG_BN_PF: 0 never prefetch, 2 always, default 1 = the shape rule in launch_bn_cfg
