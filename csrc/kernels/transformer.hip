@@ -116,7 +116,25 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
 // ds_out = ds (the residual-branch gradient); dh_out = dropout_in'(ds) (the branch gradient);
 // per-block sums of g*xhat, g (and the branch gradient, for the fused bias grad) are written as
 // partial rows and folded by ln_param_reduce_kernel.
-template <int NCH>
+//
+// Lane layout: 4-element (8-byte) chunks lane, lane + 64, ... of the H/4 chunks of a row, so H = 768 is
+// exactly 3 chunks per lane (16-byte chunks left half the lanes idle in the second pass).  The running
+// dgamma / dbeta / dbias partials live in the wave's own LDS row [3][H] (each lane only ever touches its
+// own columns, so no barrier inside the row loop), not in 36-48 accumulator registers: the kernel then
+// fits 4 waves per SIMD (it needed 158 VGPRs = 3 per SIMD, and 1024 blocks of 4 waves ran as 1.33
+// rounds of blocks).
+__device__ __forceinline__ void unpack4_bf16(const uint2 v, float (&o)[4]) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+__device__ __forceinline__ void store4_bf16(bf16_t* p, const float (&o)[4]) {
+  uint2 v;
+  v.x = pack_bf2(o[0], o[1]);
+  v.y = pack_bf2(o[2], o[3]);
+  *reinterpret_cast<uint2*>(p) = v;
+}
+
+template <int NC4>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, bf16_t* __restrict__ ds_out,
@@ -124,104 +142,97 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const bf16_t* __restrict__ 
                                                      float* __restrict__ dbias, int T, int H,
                                                      uint32_t th_in, float sc_in, uint32_t seed_in, uint32_t th_out,
                                                      float sc_out, uint32_t seed_out) {
-  extern __shared__ float red[];  // [4][3H]: gamma, beta, branch-bias partials
+  extern __shared__ float red[];  // [4][3H]: per-wave running gamma, beta, branch-bias partials
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int nc = H >> 3;
-  float dg[NCH][8], db[NCH][8], dz[NCH][8];
+  const int nc = H >> 2;
+  float4* accg = reinterpret_cast<float4*>(red + wv * 3 * H);  // chunk c of dgamma / dbeta / dbias at
+  float4* accb = accg + nc;                                    // accg[c], accb[c], accz[c]
+  float4* accz = accb + nc;
+  const bool want_z = dh_out != nullptr || dbias != nullptr;
 #pragma unroll
-  for (int j = 0; j < NCH; ++j)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) dg[j][k] = db[j][k] = dz[j][k] = 0.f;
-  // One row ahead in registers: the next row's dy / s (and its statistics) are loaded before this
-  // row's reductions and stores, so each wave keeps two rows of HBM reads in flight (2 blocks per CU
-  // leave too few waves to hide the latency otherwise).
+  for (int j = 0; j < NC4; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nc) accg[c] = accb[c] = accz[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // One row ahead in registers: the next row's dy / s (and its statistics) are loaded before this row's
+  // reductions and stores, so each wave keeps two rows of HBM reads in flight.  (Two rows ahead took 150
+  // VGPRs, 3 waves per SIMD; capped at 128 it spilled.)
   const int rstep = gridDim.x * kRowsPerBlock;
   int row = blockIdx.x * kRowsPerBlock + wv;
-  uint4 pdy[NCH], ps[NCH];
-  float pmean = 0.f, prstd = 0.f;
+  uint2 pdy[NC4], ps[NC4];
+  float pm = 0.f, pr = 0.f;
   auto prefetch = [&](int r) {
     if (r >= T) return;
     const long long b = (long long)r * H;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
+    for (int j = 0; j < NC4; ++j) {
       const int c = lane + 64 * j;
       if (c < nc) {
-        pdy[j] = *reinterpret_cast<const uint4*>(dy + b + c * 8);
-        ps[j] = *reinterpret_cast<const uint4*>(s + b + c * 8);
+        pdy[j] = *reinterpret_cast<const uint2*>(dy + b + c * 4);
+        ps[j] = *reinterpret_cast<const uint2*>(s + b + c * 4);
       }
     }
-    pmean = mean_in[r];
-    prstd = rstd_in[r];
+    pm = mean_in[r];
+    pr = rstd_in[r];
   };
   prefetch(row);
   for (; row < T; row += rstep) {
     const long long base = (long long)row * H;
-    const float mean = pmean, rstd = prstd;
-    float g[NCH][8], xh[NCH][8];
+    const float mean = pm, rstd = pr;
+    float g[NC4][4], xh[NC4][4];
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const uint4 u = pdy[j], w = ps[j];
-      g[j][0] = __uint_as_float(u.x << 16); g[j][1] = __uint_as_float(u.x & 0xffff0000u);
-      g[j][2] = __uint_as_float(u.y << 16); g[j][3] = __uint_as_float(u.y & 0xffff0000u);
-      g[j][4] = __uint_as_float(u.z << 16); g[j][5] = __uint_as_float(u.z & 0xffff0000u);
-      g[j][6] = __uint_as_float(u.w << 16); g[j][7] = __uint_as_float(u.w & 0xffff0000u);
-      xh[j][0] = __uint_as_float(w.x << 16); xh[j][1] = __uint_as_float(w.x & 0xffff0000u);
-      xh[j][2] = __uint_as_float(w.y << 16); xh[j][3] = __uint_as_float(w.y & 0xffff0000u);
-      xh[j][4] = __uint_as_float(w.z << 16); xh[j][5] = __uint_as_float(w.z & 0xffff0000u);
-      xh[j][6] = __uint_as_float(w.w << 16); xh[j][7] = __uint_as_float(w.w & 0xffff0000u);
+    for (int j = 0; j < NC4; ++j) {
+      unpack4_bf16(pdy[j], g[j]);
+      unpack4_bf16(ps[j], xh[j]);
     }
     prefetch(row + rstep);
     float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
+    for (int j = 0; j < NC4; ++j) {
       const int c = lane + 64 * j;
       if (c < nc) {
-        float gm[8];
-        load8_f32(gamma + c * 8, gm);
+        const float4 gm = *reinterpret_cast<const float4*>(gamma + c * 4);
+        const float gmv[4] = {gm.x, gm.y, gm.z, gm.w};
+        const float4 tg = accg[c], tb = accb[c];
+        float pg[4] = {tg.x, tg.y, tg.z, tg.w}, pb[4] = {tb.x, tb.y, tb.z, tb.w};
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (th_out && !keep_elem(seed_out, (uint32_t)(base + c * 8 + k), th_out)) g[j][k] = 0.f;
+        for (int k = 0; k < 4; ++k) {
+          if (th_out && !keep_elem(seed_out, (uint32_t)(base + c * 4 + k), th_out)) g[j][k] = 0.f;
           else if (th_out) g[j][k] *= sc_out;
           xh[j][k] = (xh[j][k] - mean) * rstd;
-          dg[j][k] += g[j][k] * xh[j][k];
-          db[j][k] += g[j][k];
-          g[j][k] *= gm[k];
+          pg[k] += g[j][k] * xh[j][k];
+          pb[k] += g[j][k];
+          g[j][k] *= gmv[k];
           a += g[j][k];
           b += g[j][k] * xh[j][k];
         }
+        accg[c] = make_float4(pg[0], pg[1], pg[2], pg[3]);
+        accb[c] = make_float4(pb[0], pb[1], pb[2], pb[3]);
       }
     }
     a = wave_sum(a) / H;
     b = wave_sum(b) / H;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
+    for (int j = 0; j < NC4; ++j) {
       const int c = lane + 64 * j;
       if (c < nc) {
-        float o[8];
+        float o[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[j][k] - a - xh[j][k] * b);
-        store8_bf16(ds_out + base + c * 8, o);
-        if (dh_out || dbias) {
+        for (int k = 0; k < 4; ++k) o[k] = rstd * (g[j][k] - a - xh[j][k] * b);
+        store4_bf16(ds_out + base + c * 4, o);
+        if (want_z) {
+          const float4 tz = accz[c];
+          float pz[4] = {tz.x, tz.y, tz.z, tz.w};
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            o[k] = (!th_in || keep_elem(seed_in, (uint32_t)(base + c * 8 + k), th_in)) ? o[k] * sc_in : 0.f;
-            dz[j][k] += bf2f(f2bf(o[k]));  // the bias grad of the branch = column sum of the stored dh
+          for (int k = 0; k < 4; ++k) {
+            o[k] = (!th_in || keep_elem(seed_in, (uint32_t)(base + c * 4 + k), th_in)) ? o[k] * sc_in : 0.f;
+            pz[k] += bf2f(f2bf(o[k]));  // the bias grad of the branch = column sum of the stored dh
           }
-          if (dh_out) store8_bf16(dh_out + base + c * 8, o);
+          accz[c] = make_float4(pz[0], pz[1], pz[2], pz[3]);
+          if (dh_out) store4_bf16(dh_out + base + c * 4, o);
         }
       }
     }
-  }
-#pragma unroll
-  for (int j = 0; j < NCH; ++j) {
-    const int c = lane + 64 * j;
-    if (c < nc)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        red[wv * 3 * H + c * 8 + k] = dg[j][k];
-        red[wv * 3 * H + H + c * 8 + k] = db[j][k];
-        red[wv * 3 * H + 2 * H + c * 8 + k] = dz[j][k];
-      }
   }
   __syncthreads();
   // per-block partials of [dgamma | dbeta | dbias] -> ws[block][3H]; ln_param_reduce_kernel sums them
@@ -534,14 +545,16 @@ void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* 
   const uint32_t ti = drop_thresh(p_in), to = drop_thresh(p_out);
   const float si = p_in > 0.f ? 1.f / (1.f - p_in) : 1.f, so = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
   const int nb = ln_bwd_blocks(T);
-  const int nch = (H / 8 + 63) / 64;
+  const int nc4 = (H / 4 + 63) / 64;  // 4-element chunks per lane (H = 768: 3)
   const size_t lds = (size_t)kRowsPerBlock * 3 * H * sizeof(float);
 #define DTG_LNB(NC)                                                                                                  \
   hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
                      ws, dbias, T, H, ti, si, seed_in, to, so, seed_out)
-  if (nch <= 1) DTG_LNB(1);
-  else if (nch == 2) DTG_LNB(2);
-  else DTG_LNB(4);
+  if (nc4 <= 1) DTG_LNB(1);
+  else if (nc4 == 2) DTG_LNB(2);
+  else if (nc4 == 3) DTG_LNB(3);
+  else if (nc4 == 4) DTG_LNB(4);
+  else DTG_LNB(8);
 #undef DTG_LNB
   const int ncols = dbias ? 3 * H : 2 * H;
   hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((ncols + 63) / 64, 8), dim3(256), 0, st, ws, nb, H, ncols, dgamma,
