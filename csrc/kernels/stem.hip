@@ -260,6 +260,137 @@ __global__ void __launch_bounds__(kBlk) stem_bwd_dx_kernel(const bf16_t* __restr
   }
 }
 
+// ---- backward, banded: k = 3, s = 2, pad = 1, C = 64, H % 4 == 0 (ResNet's stem) --------------------
+// One workgroup per (image, band of 4 input rows).  The pooled rows whose windows reach the band (3 rows:
+// dout + argmax, 3 x Q x 64 x 3 B = 32 KB at Q = 56) are staged in LDS once, so an input pixel's <= 4
+// candidate windows are LDS reads instead of 4 global gathers: 1.5x instead of 4x the pooled bytes move
+// through L2, and the window geometry is shift arithmetic.  DX = false: pass 1, sum(dp) and sum(dp * xhat)
+// per channel, block-reduced and added into one of kBnStatSlots zeroed slots; DX = true: pass 2,
+// dy = a*dp + bx*y + c0.
+constexpr int kStemBandRows = 4;
+
+template <bool DX>
+__global__ void __launch_bounds__(256) stem_bwd_band_kernel(const bf16_t* __restrict__ dout,
+                                                            const uint8_t* __restrict__ idx,
+                                                            const bf16_t* __restrict__ y,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            const float* __restrict__ smean,
+                                                            const float* __restrict__ sinv,
+                                                            const float* __restrict__ coef, StemGeom g,
+                                                            float* __restrict__ part, bf16_t* __restrict__ dy) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [3][Q][64] bf16 dout, then [3][Q][64] u8 argmax
+  constexpr int C = 64;
+  const int bands = g.H / kStemBandRows;
+  const int n = blockIdx.x / bands, band = blockIdx.x - n * bands;
+  const int h0 = band * kStemBandRows;
+  const int p0 = h0 >> 1;  // pooled rows p0 .. p0 + 2 (those < P) cover input rows h0 .. h0 + 3
+  bf16_t* sd = reinterpret_cast<bf16_t*>(lds);
+  uint8_t* si = reinterpret_cast<uint8_t*>(lds + 3 * g.Q * C * 2);
+  const int qc = g.Q * 8;  // 8-channel chunks per pooled row
+  for (int i = threadIdx.x; i < 3 * qc; i += 256) {
+    const int pr = i / qc;
+    if (p0 + pr < g.P) {
+      const long long o = (((long long)n * g.P + p0) * g.Q) * C + (long long)i * 8;
+      *reinterpret_cast<uint4*>(sd + i * 8) = *reinterpret_cast<const uint4*>(dout + o);
+      *reinterpret_cast<uint2*>(si + i * 8) = *reinterpret_cast<const uint2*>(idx + o);
+    }
+  }
+  const int c8 = threadIdx.x & 7, c0 = c8 * 8;  // fixed per thread: 256 is a multiple of 8 chunks
+  float sc[8], sf[8], mu[8], is[8], a[8], bx[8], cc[8];
+  {
+    float ga[8], be[8];
+    load8_f32(smean + c0, mu);
+    load8_f32(sinv + c0, is);
+    load8_f32(gamma + c0, ga);
+    load8_f32(beta + c0, be);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = ga[k] * is[k];
+      sf[k] = be[k] - mu[k] * sc[k];
+    }
+  }
+  if constexpr (DX) {
+    load8_f32(coef + c0, a);
+    load8_f32(coef + C + c0, bx);
+    load8_f32(coef + 2 * C + c0, cc);
+  }
+  __syncthreads();
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int chunks = kStemBandRows * g.W * 8;
+  for (int i = threadIdx.x; i < chunks; i += 256) {
+    const int pix = i >> 3;
+    const int hr = pix / g.W, w = pix - hr * g.W;
+    const int h = h0 + hr;
+    const long long off = (((long long)n * g.H + h) * g.W + w) * C + c0;
+    float yv[8];
+    load8_bf16(y + off, yv);
+    const int hp = h + 1, wp = w + 1;  // padded coordinates
+    const int p_hi = min(g.P - 1, hp >> 1), q_hi = min(g.Q - 1, wp >> 1);
+    const int p_lo = hp >= 3 ? ((hp - 3) >> 1) + 1 : 0, q_lo = wp >= 3 ? ((wp - 3) >> 1) + 1 : 0;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = p_hi - 1 + (j >> 1), qq = q_hi - 1 + (j & 1);
+      if (p >= p_lo && qq >= q_lo) {
+        const int li = ((p - p0) * g.Q + qq) * C + c0;
+        const uint4 dv = *reinterpret_cast<const uint4*>(sd + li);
+        const uint2 pk = *reinterpret_cast<const uint2*>(si + li);
+        const uint32_t wi = (uint32_t)((hp - 2 * p) * 3 + (wp - 2 * qq));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t word = k < 4 ? pk.x : pk.y;
+          const uint32_t pair = (k >> 1) == 0 ? dv.x : (k >> 1) == 1 ? dv.y : (k >> 1) == 2 ? dv.z : dv.w;
+          const float d = __uint_as_float((k & 1) ? (pair & 0xffff0000u) : (pair << 16));
+          acc[k] += ((word >> (8 * (k & 3))) & 0xffu) == wi ? d : 0.f;
+        }
+      }
+    }
+    float dp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dp[k] = fmaf(yv[k], sc[k], sf[k]) > 0.f ? acc[k] : 0.f;
+    if constexpr (DX) {
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], dp[k], fmaf(bx[k], yv[k], cc[k]));
+      store8_bf16(dy + off, o);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += dp[k];
+        q[k] += dp[k] * (yv[k] - mu[k]) * is[k];
+      }
+    }
+  }
+  if constexpr (!DX) {
+    __syncthreads();  // the staged rows are no longer read: reuse the LDS for the block reduction
+    float* red = reinterpret_cast<float*>(lds);  // [2][32 thread rows][64 channels]
+    const int r = threadIdx.x >> 3;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[r * C + c0 + k] = s[k];
+      red[32 * C + r * C + c0 + k] = q[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float ts = 0.f, tq = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < 32; ++j) {
+        ts += red[j * C + threadIdx.x];
+        tq += red[32 * C + j * C + threadIdx.x];
+      }
+      float* slot = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * C;
+      atomicAdd(slot + threadIdx.x, ts);
+      atomicAdd(slot + C + threadIdx.x, tq);
+    }
+  }
+}
+
+static bool stem_band_ok(int H, int C, int k, int s, int pad, int P) {
+  static const bool on = !getenv("DTG_STEM_BAND") || atoi(getenv("DTG_STEM_BAND")) != 0;
+  return on && k == 3 && s == 2 && pad == 1 && C == 64 && H % kStemBandRows == 0 && P == (H - 1) / 2 + 1;
+}
+
 // ---- input packing for the pixel-pair stem conv (ops/conv.py stem_pairs) ---------------------------
 // x [N, H, W, C] (C <= 4, NHWC bf16) -> xp [N, H + 2*pad, Wp, 4] zero-padded (pad rows/columns on the
 // top/left, the rest on the bottom/right, channels C..3 zero): one thread per 16-byte output chunk
@@ -350,6 +481,19 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   float* part = ws;
   float* coef = ws + (long long)bg.nchunk * 2 * C;
+  if (stem_band_ok(H, C, k, s, pad, P) && bg.nchunk >= kBnStatSlots) {
+    const size_t lds = (size_t)3 * Q * C * 3 > (size_t)2 * 32 * C * 4 ? (size_t)3 * Q * C * 3 : (size_t)2 * 32 * C * 4;
+    const unsigned nb = (unsigned)(N * (H / kStemBandRows));
+    DTG_HIP_CHECK(hipMemsetAsync(part, 0, (size_t)kBnStatSlots * 2 * C * sizeof(float), st));
+    hipLaunchKernelGGL(stem_bwd_band_kernel<false>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
+                       sinv, nullptr, g, part, nullptr);
+    bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr,
+                                                           nullptr, nullptr, const_cast<float*>(smean),
+                                                           const_cast<float*>(sinv), 0.f, 0.f, coef, dgamma, dbeta);
+    hipLaunchKernelGGL(stem_bwd_band_kernel<true>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
+                       sinv, coef, g, nullptr, dy);
+    return;
+  }
   dim3 grid(bg.nchunk, bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_reduce_kernel<T><<<grid, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, g, M,
                                                                          bg.rows_per_chunk, part));

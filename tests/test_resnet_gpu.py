@@ -163,19 +163,21 @@ def test_wgrad_side_stream_matches_main_stream(monkeypatch):
     assert max(errs) < 1e-2, errs
 
 
+@pytest.mark.parametrize("size", [64, 60])
 @pytest.mark.parametrize("pairs", ["1", "0"])
 @pytest.mark.parametrize("flat", [False, True])
-def test_fused_stem_matches_unfused(flat, pairs, monkeypatch):
+def test_fused_stem_matches_unfused(flat, pairs, size, monkeypatch):
     """conv7x7/2 -> BN -> ReLU -> maxpool3x3/2 as one node (csrc/kernels/stem.hip: BN statistics from the
     conv epilogue, BN+ReLU+pool in one pass, gather-form backward) equals the op-by-op path: output,
-    running statistics and the conv / gamma / beta gradients."""
+    running statistics and the conv / gamma / beta gradients.  size 64 (conv output 32x32, a multiple of
+    4 rows) runs the LDS-banded backward, size 60 (30x30) the per-pixel gather form."""
     from dtg.models.layers import ConvBN
     from dtg.models import resnet_fused
     from dtg.ops.pool import max_pool2d
     monkeypatch.setenv("DTG_STEM_PAIRS", pairs)  # pixel-pair (ops/conv.py stem_pairs) or 8-channel stem conv
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1)
-    x = torch.randn(4, 3, 64, 64, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, size, size, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     res = []
     for fused in (False, True):
         monkeypatch.setattr(resnet_fused, "_STEM", fused)
