@@ -771,7 +771,8 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp,
 }
 
 // dw (+)= wgrad; dw is [K, R, S, C] contiguous, fp32 or bf16 (beta = 1 accumulates into a flat grad)
-void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad, int64_t stride_w) {
+void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad, int64_t stride_w,
+                int64_t target_wgs) {
   check_nhwc(dy, "dy");
   check_nhwc(x, "x");
   CHECK_CUDA(dw);
@@ -785,7 +786,7 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
   const int P = (H + 2 * pad - R) / stride + 1, Q = (W + 2 * pad - S) / sw + 1;
   TORCH_CHECK(dy.size(1) == P && dy.size(2) == Q, "wgrad geometry mismatch");
   c10::DeviceGuard dg(x.device());
-  const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad, sw);
+  const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad, sw, (int)target_wgs);
   auto ws = at::empty({(long long)split * K * R * S * C}, x.options().dtype(at::kFloat));
   dtg::conv_wgrad(cbfp(dy), cbfp(x), dw.data_ptr(), dw.scalar_type() == at::kBFloat16, (float)beta,
                   ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw);
@@ -803,7 +804,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("out") = pybind11::none(),
         pybind11::arg("beta") = 0.0, pybind11::arg("zero_rest") = true);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"),
-        pybind11::arg("beta"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stride_w") = 0);
+        pybind11::arg("beta"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stride_w") = 0,
+        pybind11::arg("target_wgs") = 0);
   m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),
@@ -848,6 +850,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
   m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });
   m.def("softmax_xent_bwd", &softmax_xent_bwd);
+  m.def("gemm_pick_split", [](int64_t M, int64_t N, int64_t K, bool a_kc, int64_t target_wgs) {
+    return dtg::gemm_pick_split((int)M, (int)N, (int)K, a_kc ? 1 : 0, (int)target_wgs);
+  }, pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("a_kc") = false,
+        pybind11::arg("target_wgs") = 0);
   m.def("gemm", &gemm, pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"), pybind11::arg("b_kc"),
         pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 0,

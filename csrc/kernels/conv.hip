@@ -596,14 +596,16 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
   return 1;
 }
 
-int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
+int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w,
+                     int target_wgs) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   const long long tiles = K <= 64 ? (long long)((No + 255) / 256) : (long long)((K + 127) / 128) * ((No + 127) / 128);
   // target workgroups (DTG_WGRAD_BLOCKS, default 1024 = 4 single-stage workgroups per CU; measured 3-5 %
   // faster than 512 on the 14x14 / 28x28 3x3 layers, 256 is 25 % slower); more splits also grow the fp32
   // slabs the reduce pass re-reads
-  static const long long target = getenv("DTG_WGRAD_BLOCKS") ? atoll(getenv("DTG_WGRAD_BLOCKS")) : 1024;
+  static const long long dflt = getenv("DTG_WGRAD_BLOCKS") ? atoll(getenv("DTG_WGRAD_BLOCKS")) : 1024;
+  const long long target = target_wgs > 0 ? target_wgs : dflt;
   // up to 1024 splits when the fp32 slabs stay small (<= 64 MB): the stem's single 64 x 224 output tile
   // needs 1024 splits to reach 1024 workgroups (at 256 it ran 256 workgroups, one per CU)
   const long long slab = (long long)K * No * 4;

@@ -94,7 +94,7 @@ static bool skinny(int N) { return N <= 64; }
 
 static bool short_m(int M, int N) { return M <= 64 && N >= 128; }
 
-int gemm_pick_split(int M, int N, int K, int a_kc) {
+int gemm_pick_split(int M, int N, int K, int a_kc, int target_wgs) {
   const int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   // forward / data-gradient GEMMs (K-contiguous A) with >= 128 tiles: the fp32 partial round trip
@@ -110,9 +110,11 @@ int gemm_pick_split(int M, int N, int K, int a_kc) {
     return s;
   }
   int s = 1;
-  // aim for >= ~512 workgroups (2 per CU: the LDS ring admits 2) while keeping >= 1024 K
-  // (16 K-steps) per split
-  while (tiles * s < 512 && (long long)K / (s * 2) >= 1024 && s < 256) s *= 2;
+  // aim for >= ~512 workgroups while keeping >= 1024 K (16 K-steps) per split (DTG_GEMM_SPLIT_WGS
+  // overrides the workgroup target for A/B runs)
+  static const long long dflt = getenv("DTG_GEMM_SPLIT_WGS") ? atoll(getenv("DTG_GEMM_SPLIT_WGS")) : 512;
+  const long long target = target_wgs > 0 ? target_wgs : dflt;
+  while (tiles * s < target && (long long)K / (s * 2) >= 1024 && s < 256) s *= 2;
   return s;
 }
 

@@ -88,6 +88,33 @@ def _gacc(p):
 _BITS = os.environ.get("DTG_BN_BITS", "1") != "0"
 
 
+# Split-K targets (workgroups) of the weight gradients when they run on the side stream (parallel/overlap.py,
+# one rank): there they overlap the dgrad / BN-backward chain, and fewer, longer splits (fewer fp32 partial
+# slabs, fewer CUs taken from the main stream) measured faster -- ResNet-50 b512 13.99k -> 14.19k img/s
+# for the 1x1 GEMM wgrads at 128 instead of 512, and +0.7 % for the 3x3 conv wgrads at 512 instead of
+# 1024.  On the main stream (several ranks, or DTG_WGRAD_STREAM=0) the kernels' own defaults stay: there
+# 128 ran 12.4k vs 13.67k img/s (profiles/r02_wgrad_split_policy).  DTG_RESNET_WSPLIT_WGS /
+# DTG_RESNET_CWSPLIT_WGS override the side-stream targets (0: the defaults).
+_WSPLIT_WGS = int(os.environ.get("DTG_RESNET_WSPLIT_WGS", "128"))
+_CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "512"))
+_wsplit_cache = {}
+
+
+def _wgrad(dy, x, out):
+    """out (+)= dy^T x for [P, M] dy and [P, N] x (P pixels): a 1x1 conv weight gradient."""
+    tgt = _WSPLIT_WGS if overlap.enabled() else 0
+    key = (dy.shape[1], x.shape[1], dy.shape[0], tgt)
+    sk = _wsplit_cache.get(key)
+    if sk is None:
+        sk = _wsplit_cache[key] = lib().gemm_pick_split(key[0], key[1], key[2], False, tgt) if tgt > 0 else 0
+    gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
+
+
+def _conv_wgrad(dy4, x4, dw, st, pad):
+    """dw (+)= 3x3 / strided conv weight gradient, with the side-stream split target (see above)."""
+    lib().conv_wgrad(dy4, x4, dw, 1.0, st, pad, target_wgs=_CWSPLIT_WGS if overlap.enabled() else 0)
+
+
 def _relu_bits(y):
     return torch.empty(y.shape[0], y.shape[1] // 8, device=y.device, dtype=torch.uint8) if _BITS else None
 
@@ -213,7 +240,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
         with overlap.wgrad_scope(dy3, a2):
-            gemm(dy3, False, a2, False, out=g[id(w3)].view(cout, width), beta=1.0)
+            _wgrad(dy3, a2, g[id(w3)].view(cout, width))
         # BN2 + conv2 (3x3)
         if _FUSE:
             dy2 = L.bn_bwd_part(dp2, y2, q2, b2.weight, m2, i2, False, g[id(b2.weight)], g[id(b2.bias)])[0]
@@ -227,7 +254,7 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             da1 = L.conv_dgrad(dy2_4, _krsc(w2).contiguous(), h, w, st, 1).view(-1, width)
         with overlap.wgrad_scope(dy2_4, a1):
-            L.conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), 1.0, st, 1)
+            _conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), st, 1)
         # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
         if _FUSE:
             dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
@@ -248,7 +275,7 @@ class _BottleneckFn(torch.autograd.Function):
             if st == 1:
                 dx2 = gemm(dyd, True, _mat(wd), False)
                 with overlap.wgrad_scope(dyd, x2):
-                    gemm(dyd, False, x2, False, out=g[id(wd)].view(cout, c), beta=1.0)
+                    _wgrad(dyd, x2, g[id(wd)].view(cout, c))
             elif lk_in is not None:  # projection dgrad first, so the conv1 dgrad GEMM is the last writer
                 # only the even (h, w) rows of a stride-2 1x1 dgrad are written; the mode-3 GEMM below reads
                 # just those (sub2_hw) instead of a zero-filled full tensor
@@ -258,16 +285,14 @@ class _BottleneckFn(torch.autograd.Function):
                 if sub2:
                     sub2_hw = (h, w)
                 with overlap.wgrad_scope(dyd, x2):
-                    L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
-                                 st, 0)
+                    _conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), st, 0)
             else:
                 dx2 = gemm(dy1, True, _mat(w1), False)
                 L.conv_dgrad(dyd.view(n, p_, q_, cout), _krsc(wd).contiguous(), h, w, st, 0, out=dx2.view(n, h, w, c),
                              beta=1.0)
                 dx_done = True
                 with overlap.wgrad_scope(dyd, x2):
-                    L.conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), 1.0,
-                                 st, 0)
+                    _conv_wgrad(dyd.view(n, p_, q_, cout), x2.view(n, h, w, c), g[id(wd)].permute(0, 2, 3, 1), st, 0)
         else:
             dx2 = dres
         if not dx_done:
@@ -282,7 +307,7 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
         with overlap.wgrad_scope(dy1, x2):
-            gemm(dy1, False, x2, False, out=g[id(w1)].view(width, c), beta=1.0)
+            _wgrad(dy1, x2, g[id(w1)].view(width, c))
         grads = []
         for p, (a, direct) in zip(params, accs):
             if direct:
