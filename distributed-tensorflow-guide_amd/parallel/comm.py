@@ -34,7 +34,10 @@ def init(backend=None, timeout_s=600):
         torch.cuda.set_device(device)
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    # DTG_DDP_FORCE=1: a process group (and DataParallel's bucket hooks, parallel/ddp.py) even at world size
+    # 1 -- a one-rank RCCL communicator exercises the collective / stream interplay on a one-GPU box
+    force = os.environ.get("DTG_DDP_FORCE") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {}

@@ -17,6 +17,8 @@ Design:
   ~1 TB/s aggregate xGMI rate, small enough that ResNet-50's 51 MB of bf16 gradients forms 2
   buckets that start before backward ends (sweep with ``bucket_mb``).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -45,7 +47,10 @@ class DataParallel:
         self.flat = flat
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.overlap = overlap and self.world > 1
+        forced = os.environ.get("DTG_DDP_FORCE") == "1" and dist.is_available() and dist.is_initialized()
+        self.overlap = overlap and (self.world > 1 or forced)
+        self._force = forced
+        self._cstreams = {}
         self.buckets = []
         self._hooks = []
         cap = int(bucket_mb * (1 << 20))
@@ -84,13 +89,30 @@ class DataParallel:
     def _launch(self, b):
         v = b.view()
         side = overlap.pending_stream(v)
-        if side is not None:
-            # weight gradients of this bucket may still be running on a side stream (parallel/overlap.py;
-            # single-rank only by default): the main stream waits for them (an event, no host sync) and the
-            # collective is enqueued from the main stream exactly as without the side stream
-            torch.cuda.current_stream(v.device).wait_stream(side)
         with trace_range("dtg.allreduce.bucket%d" % b.index):  # roctx range (DTG_TRACE=1)
+            if side is not None and dist.get_backend(self.pg) == "nccl":
+                # weight gradients of this bucket may still be running on the side stream (parallel/overlap.py),
+                # its BN-parameter gradients come from main-stream kernels.  The collective is enqueued from a
+                # third stream that waits for both (events at this point of each queue): RCCL's stream waits
+                # for that one, and neither the dgrad / BN-backward chain nor the wgrad stream stalls.
+                main = torch.cuda.current_stream(v.device)
+                cs = self._comm_stream(v.device)
+                cs.wait_stream(main)
+                cs.wait_stream(side)
+                with torch.cuda.stream(cs):
+                    b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                return
+            if side is not None:
+                # host-staged backends (gloo): the main stream waits for the side stream (an event, no host
+                # sync) and the collective is enqueued from the main stream exactly as without it
+                torch.cuda.current_stream(v.device).wait_stream(side)
             b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+    def _comm_stream(self, device):
+        cs = self._cstreams.get(device.index)
+        if cs is None:
+            cs = self._cstreams[device.index] = torch.cuda.Stream(device=device)
+        return cs
 
     def _on_direct(self, p):
         if p in self._param_bucket:
@@ -117,7 +139,7 @@ class DataParallel:
     def finish(self):
         """Wait for every bucket's all-reduce (launching any that did not fire)."""
         overlap.join()  # (normally already joined at the end of backward)
-        if self.world == 1:
+        if self.world == 1 and not self._force:
             return
         for b in self.buckets:
             if b.work is None:

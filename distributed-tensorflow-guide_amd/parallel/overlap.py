@@ -21,18 +21,27 @@ independent kernels instead of one.
 * a gradient all-reduce launched during backward (parallel/ddp.py) first makes the main stream wait
   for the side stream (an event, no host sync), then is enqueued from the main stream as usual.
 
-Single-process only: with more than one rank the weight gradients stay on the main stream.  The
-two-rank rehearsal on one card (gloo, both ranks on cuda:0) ran 9-40x slower with the side stream
-than without it (profiles/r02_overlap), whichever stream enqueued the collectives.  A likely cause is
-the extra stream oversubscribing the per-process hardware queues (4 per process on the box) next to
-the collective library's own streams.  The one-GPU-per-rank RCCL case cannot be measured here, so
-the multi-rank path keeps round 1's validated stream pattern.
+Several ranks: the main stream only, by default.  The opt-in form (``DTG_WGRAD_STREAM=2``) enqueues a
+bucket's collective from a third stream that waits for both the main and the side stream
+(parallel/ddp.py), so neither stalls.  That needs at least 8 hardware queues per process
+(``GPU_MAX_HW_QUEUES=8``): with HIP's default of 4, the main, side, collective and RCCL streams share
+hardware queues and their kernels serialise.  A one-rank RCCL process group (``DTG_DDP_FORCE=1``) on one
+GPU shows it (ResNet-50 b512, profiles/r02_side_stream_ddp):
 
-``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs); ``=2`` uses the side stream with
-several ranks too.  Measured gain on one rank:
-ResNet-50 +2.3 %, BERT-base +1.1 %.  The record_stream version once ran a whole bench 5x slower
-(191 ms/step instead of 37 ms, same losses), most likely because its allocator reserve kept growing
-(profiles/r02_overlap).
+- main stream only: 13.96k img/s;
+- side stream at 4 queues: 12.37k;
+- side stream at 8 queues: 14.48k (no process group at all: 14.58k).
+
+It stays opt-in because the one-GPU-per-rank RCCL case cannot be run from here, and 8 queues per process
+hung the two-rank gloo rehearsal, where both ranks share one card.  gloo (host-staged) always keeps the
+wgrads on the main stream: there the side stream ran 9-40x slower (profiles/r02_overlap), because the
+staging copies synchronise the host.
+
+``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).  ``=2`` forces the side stream
+with several ranks, whatever the backend and queue count.  Measured gain on one rank:
+ResNet-50 +2.3 % (+4 % with the side-stream split targets of models/resnet_fused.py), BERT-base +1.1 %.
+The record_stream version once ran a whole bench 5x slower (191 ms/step instead of 37 ms, same losses),
+most likely because its allocator reserve kept growing (profiles/r02_overlap).
 """
 import contextlib
 import os

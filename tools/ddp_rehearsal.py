@@ -32,7 +32,7 @@ def main():
     from dtg.parallel import DataParallel, FlatParams, comm
 
     rank, _, world, device = comm.init()
-    assert device.type == "cuda" and world > 1
+    assert device.type == "cuda" and (world > 1 or os.environ.get("DTG_DDP_FORCE") == "1")
     ops.lib()
     torch.manual_seed(7)
     if a.model == "resnet":
