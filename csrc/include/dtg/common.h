@@ -45,6 +45,15 @@ __device__ __forceinline__ void store8_bf16(bf16_t* p, const float (&o)[8]) {
   *reinterpret_cast<uint4*>(p) = v;
 }
 
+// store8_bf16 with a non-temporal hint: for tensors read again only much later (saved for backward)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
+__device__ __forceinline__ void store8_bf16_nt(bf16_t* p, const float (&o)[8]) {
+  u32x4v v;
+  v.x = pack_bf2(o[0], o[1]); v.y = pack_bf2(o[2], o[3]);
+  v.z = pack_bf2(o[4], o[5]); v.w = pack_bf2(o[6], o[7]);
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(p));
+}
+
 __device__ __forceinline__ void load8_f32(const float* p, float (&o)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p);
   const float4 b = *reinterpret_cast<const float4*>(p + 4);

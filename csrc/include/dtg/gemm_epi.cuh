@@ -153,7 +153,9 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
       d[k] = fmaf(2.f * x * sg * (1.f - sg), du, sg);
       v[k] = x * sg;
     }
-    store8_bf16((bf16_t*)e.aux + off, d);
+    // GELU'(pre) is read again only in the backward pass: a non-temporal store keeps it from evicting
+    // the activation the next GEMM reads at once from the Infinity Cache
+    store8_bf16_nt((bf16_t*)e.aux + off, d);
   } else if (e.act == 1) {
     if (e.aux_mode == 3) {
       float d[8];

@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const bf16_t* __restrict__ 
         v[j][k] = bf2f(f2bf(v[j][k]));  // statistics of the stored (bf16) sum
         sum += v[j][k];
       }
-      if (s_out) store8_bf16(s_out + base + c * 8, v[j]);
+      // read again only in backward: non-temporal, so it does not evict what the next GEMM reads
+      if (s_out) store8_bf16_nt(s_out + base + c * 8, v[j]);
     }
   }
   const float mean = wave_sum(sum) / H;
