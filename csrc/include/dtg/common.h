@@ -54,6 +54,16 @@ __device__ __forceinline__ void store8_bf16_nt(bf16_t* p, const float (&o)[8]) {
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(p));
 }
 
+// load8_bf16 with a non-temporal hint: the last read of a tensor in this step (its lines are evicted first,
+// so freshly written data that the next kernel reads stays in the caches)
+__device__ __forceinline__ void load8_bf16_nt(const bf16_t* p, float (&o)[8]) {
+  const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p));
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  o[4] = __uint_as_float(v.z << 16); o[5] = __uint_as_float(v.z & 0xffff0000u);
+  o[6] = __uint_as_float(v.w << 16); o[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
 __device__ __forceinline__ void load8_f32(const float* p, float (&o)[8]) {
   const float4 a = *reinterpret_cast<const float4*>(p);
   const float4 b = *reinterpret_cast<const float4*>(p + 4);

@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // NHWC BatchNorm for training, fused with the residual add and ReLU that follow it in ResNet
 // bottlenecks:   y = relu( (x - mean) * invstd * gamma + beta  [+ residual] )
 //
@@ -238,7 +239,7 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_reduce_kernel(const bf16_t* __res
 }
 
 // ---- pass 2 (bwd): dx = a*dp + bx*x + c0 ; dres = dp ------------------------------------------
-template <int TPR, bool RELU, bool DRES>
+template <int TPR, bool RELU, bool DRES, bool NT = true>
 __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                          const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
@@ -268,10 +269,19 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
   for (; m + RPP < m1; m += 2 * RPP) {  // 2 rows per iteration, up to six 16-B loads in flight
     const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
     float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
-    load8_bf16(dy + o0, g0);
-    load8_bf16(dy + o1, g1);
-    load8_bf16(x + o0, x0);
-    load8_bf16(x + o1, x1);
+    // dp and the saved BN input are read for the last time in this step: non-temporal, so the dx written
+    // here stays cached for the dgrad / wgrad GEMMs that read it next
+    if constexpr (NT) {
+      load8_bf16_nt(dy + o0, g0);
+      load8_bf16_nt(dy + o1, g1);
+      load8_bf16_nt(x + o0, x0);
+      load8_bf16_nt(x + o1, x1);
+    } else {
+      load8_bf16(dy + o0, g0);
+      load8_bf16(dy + o1, g1);
+      load8_bf16(x + o0, x0);
+      load8_bf16(x + o1, x1);
+    }
     if constexpr (RELU) {
       load8_bf16(y + o0, y0);
       load8_bf16(y + o1, y1);
@@ -282,11 +292,21 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
   if (m < m1) {
     const long long o0 = m * C + c0;
     float g0[8], x0[8], y0[8];
-    load8_bf16(dy + o0, g0);
-    load8_bf16(x + o0, x0);
+    if constexpr (NT) {
+      load8_bf16_nt(dy + o0, g0);
+      load8_bf16_nt(x + o0, x0);
+    } else {
+      load8_bf16(dy + o0, g0);
+      load8_bf16(x + o0, x0);
+    }
     if constexpr (RELU) load8_bf16(y + o0, y0);
     finish(g0, x0, y0, o0);
   }
+}
+
+static bool bn_nt_loads() {
+  static const bool on = !getenv("DTG_BN_NT") || atoi(getenv("DTG_BN_NT")) != 0;
+  return on;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -466,7 +486,10 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
-    if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+    if (!bn_nt_loads()) {  // DTG_BN_NT=0: plain loads (A/B)
+      if (dres) bn_bwd_dx_kernel<T, false, true, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+      else bn_bwd_dx_kernel<T, false, false, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+    } else if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
     else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
   });
 }
