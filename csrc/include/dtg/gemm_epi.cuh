@@ -136,7 +136,7 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
   if (e.aux_mode == 1) store8_bf16((bf16_t*)e.aux + off, v);
   if (e.aux_mode == 2 || e.aux_mode == 4) {
     float pre[8];
-    load8_bf16((const bf16_t*)e.aux + off, pre);
+    load8_bf16_nt((const bf16_t*)e.aux + off, pre);  // saved in forward, last use
     if (e.aux_mode == 4) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] *= pre[k];
