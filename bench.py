@@ -56,6 +56,29 @@ def parse(argv=None):
     return ap.parse_known_args(argv)[0]
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _self_launch(n, argv):
+    """``python bench.py --gpus N`` (N > 1) outside torchrun: start the N rank processes here, one per GPU,
+    through torch.distributed.run on 127.0.0.1, before this process touches the GPU (nothing above has
+    imported torch).  Rank 0's JSON line reaches our stdout unchanged; the exit code is torchrun's, which is
+    non-zero when any rank fails.  Reference semantics: one process per replica, all replicas aggregated
+    every step (Synchronous-SGD/ssgd.py:51-55)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def _backend_name():
     """'rccl' for the production path (torch's "nccl" backend is RCCL on ROCm), else the backend."""
     import torch.distributed as dist
@@ -65,6 +88,8 @@ def _backend_name():
 
 def main(argv=None):
     a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(a.gpus, sys.argv[1:] if argv is None else argv))
     import torch
     import dtg  # noqa: F401
     from dtg.models import resnet
@@ -89,8 +114,10 @@ def main(argv=None):
 
     rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
     a.bucket_mb = a.bucket_mb or (25.0 if a.model == "bert" else 8.0)
-    if world != a.gpus and rank == 0:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != a.gpus:
+        # a mislabelled point on the scaling curve is worse than no point
+        comm.shutdown()
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     torch.manual_seed(1234)
     if device.type == "cuda":
         ops.lib()  # fail loudly if the HIP kernels are missing

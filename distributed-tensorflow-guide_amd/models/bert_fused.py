@@ -44,6 +44,10 @@ def _gacc(p):
 
 
 def _finish(params, accs, skip_notify=()):
+    if not all(direct for _, direct in accs):
+        # gradients without a flat buffer may have been written on the wgrad side stream: autograd can add
+        # them into an existing .grad on the current stream as soon as we return them
+        overlap.sync_current(accs[0][0].device)
     grads = []
     for p, (a, direct) in zip(params, accs):
         if direct:

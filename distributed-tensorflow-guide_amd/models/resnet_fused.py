@@ -308,6 +308,8 @@ class _BottleneckFn(torch.autograd.Function):
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
         with overlap.wgrad_scope(dy1, x2):
             _wgrad(dy1, x2, g[id(w1)].view(width, c))
+        if not all(direct for _, direct in accs):
+            overlap.sync_current(x2.device)  # side-stream wgrads land in these before autograd adds them
         grads = []
         for p, (a, direct) in zip(params, accs):
             if direct:

@@ -13,9 +13,10 @@ Design:
   waits on the compute stream's event at launch, so it overlaps the rest of backward;
 * ``finish()`` joins all outstanding collectives into the compute stream; the 1/world averaging is
   folded into the optimizer's gradient scale (no separate divide kernel);
-* bucket size default 32 MB: large enough to amortise the ~tens-of-µs RCCL launch against the
-  ~1 TB/s aggregate xGMI rate, small enough that ResNet-50's 51 MB of bf16 gradients forms 2
-  buckets that start before backward ends (sweep with ``bucket_mb``).
+* bucket size (constructor default 32 MB; bench.py passes 8 MB for ResNet-50 and 25 MB for BERT): large
+  enough to amortise the ~tens-of-µs RCCL launch against the xGMI link rate, small enough that the
+  last bucket -- the only one left to reduce after backward ends -- is short (sweep with
+  ``tools/allreduce_bw.py`` and ``bench.py --bucket_mb``).
 """
 import os
 
@@ -24,6 +25,8 @@ import torch.distributed as dist
 
 from . import grad_sink, overlap
 from ..utils.trace import trace_range
+
+_LAUNCH = os.environ.get("DTG_DDP_LAUNCH", "side")  # stream a bucket's collective is enqueued from
 
 
 class _Bucket:
@@ -92,14 +95,19 @@ class DataParallel:
         with trace_range("dtg.allreduce.bucket%d" % b.index):  # roctx range (DTG_TRACE=1)
             if side is not None and dist.get_backend(self.pg) == "nccl":
                 # weight gradients of this bucket may still be running on the side stream (parallel/overlap.py),
-                # its BN-parameter gradients come from main-stream kernels.  The collective is enqueued from a
-                # third stream that waits for both (events at this point of each queue): RCCL's stream waits
-                # for that one, and neither the dgrad / BN-backward chain nor the wgrad stream stalls.
+                # its BN-parameter gradients come from main-stream kernels.  The side stream waits for the
+                # main stream's event at this point and the collective is enqueued FROM the side stream, so
+                # RCCL's stream waits for both.  No third stream: main + side + RCCL's own stream fit the four
+                # hardware queues a HIP process gets by default (GPU_MAX_HW_QUEUES=4), where a separate
+                # launch stream made two streams share a queue and serialise (profiles/r03_streams).  The
+                # side stream's later wgrads need the main stream's later dgrads anyway, so the wait costs
+                # it nothing.  DTG_DDP_LAUNCH=comm restores the third stream (A/B).
                 main = torch.cuda.current_stream(v.device)
-                cs = self._comm_stream(v.device)
-                cs.wait_stream(main)
-                cs.wait_stream(side)
-                with torch.cuda.stream(cs):
+                ls = self._comm_stream(v.device) if _LAUNCH == "comm" else side
+                ls.wait_stream(main)
+                if ls is not side:
+                    ls.wait_stream(side)
+                with torch.cuda.stream(ls):
                     b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
                 return
             if side is not None:

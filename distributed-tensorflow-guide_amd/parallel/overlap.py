@@ -54,15 +54,18 @@ _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()
 _keep = {}      # device index -> tensors the side stream reads, released at the join
+_cb_task = {}   # device index -> autograd graph task whose end-of-backward callback joins it
 
 
-def _multi_rank():
+def _host_staged_multi_rank():
+    """Several ranks on a backend that stages collectives through host memory (gloo)."""
     import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            and dist.get_backend() != "nccl")
 
 
 def enabled():
-    return _ON and (_MULTI or not _multi_rank())
+    return _ON and (_MULTI or not _host_staged_multi_rank())
 
 
 def set_enabled(on):
@@ -97,13 +100,17 @@ def wgrad_scope(*tensors):
     main = torch.cuda.current_stream(t0.device)
     side = side_stream(t0.device)
     side.wait_stream(main)
+    if idx in _pending and _main[idx] != main:
+        _join(idx)  # left over from a scope under another stream: settle it first
     if idx not in _pending:
         _pending.add(idx)
         _main[idx] = main
-        try:  # join at the end of this backward pass
-            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
-        except RuntimeError:  # not inside a backward pass: the caller joins (join())
-            pass
+    # one end-of-backward join per backward pass (graph task): a scope entered outside backward, or a
+    # backward that raised before its callback ran, must not stop later passes from queueing theirs
+    task = torch._C._current_graph_task_id()
+    if task >= 0 and _cb_task.get(idx) != task:
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
+        _cb_task[idx] = task
     _keep.setdefault(idx, []).extend(t for t in tensors if t is not None)
     with torch.cuda.stream(side):
         yield
@@ -115,6 +122,18 @@ def pending_stream(t):
         return None
     idx = t.device.index
     return _side[idx] if idx in _pending else None
+
+
+def sync_current(device):
+    """Make the current stream wait for the side stream's queued work on ``device`` (an event, no host
+    sync) without ending the backward's pending set.  For gradients handed to autograd from inside a
+    backward (parameters without a flat gradient buffer): AccumulateGrad may add them into an existing
+    ``.grad`` on the current stream right away."""
+    if device.type != "cuda":
+        return
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx in _pending:
+        torch.cuda.current_stream(device).wait_stream(_side[idx])
 
 
 def join(device=None):

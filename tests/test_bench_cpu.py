@@ -1,0 +1,45 @@
+"""bench.py's launch contract on the CPU (gloo): ``python bench.py --gpus N`` starts N ranks by itself and
+reports the whole job, and a launcher whose world size disagrees with ``--gpus`` is a hard error."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--model", "mnist", "--batch", "4", "--steps", "2", "--warmup", "1"]
+
+
+def _env(**kw):
+    e = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "DTG_DDP_FORCE"):
+        e.pop(k, None)
+    e.update(kw)
+    return e
+
+
+def _json_line(out):
+    rows = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+    assert len(rows) == 1, out  # rank 0 only
+    return rows[0]
+
+
+def test_plain_gpus2_self_launches_two_ranks():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL, cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    j = _json_line(r.stdout)
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2", j
+    assert j["config"]["global_batch"] == 8 and j["steps"] == 2 and j["warmup"] == 1
+    assert j["value"] > 0 and j["ms_per_step"] > 0
+
+
+def test_world_size_mismatch_is_an_error():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "4"] + SMALL
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
+    assert not any(x.startswith("{") for x in r.stdout.splitlines())

@@ -206,3 +206,31 @@ def test_aemasgd_two_workers_converge():
     center_line = [l for l in out[("worker", 0)][1].splitlines() if l.startswith("center")][-1]
     vals = [float(x) for x in center_line.split("[")[1].split("]")[0].split()]
     assert all(abs(v - 100.0) < 5.0 for v in vals), vals
+
+
+def test_notebook_shared_ps_protocol():
+    """Basics-Tutorial/Multiple-Workers through its run.sh: both workers move the ONE shared `g/a` on the PS,
+    +0.1 per global update whichever worker applies it (Local-then-Global-Variables-Worker1.ipynb:224, :286,
+    :313 and -Worker2.ipynb:217, :286: -1.17584 -> -1.07584 -> -0.97584); every task exits 0."""
+    import json
+    import re
+    import subprocess
+    from _cluster import ROOT, free_ports
+    ports = free_ports(3)
+    spec = {"ps": ["127.0.0.1:%d" % ports[0]], "worker": ["127.0.0.1:%d" % p for p in ports[1:]]}
+    sh = os.path.join(ROOT, "examples", "Basics-Tutorial", "Multiple-Workers", "run.sh")
+    p = subprocess.run(["bash", sh, "--cluster", json.dumps(spec)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert p.returncode == 0, p.stdout + p.stderr
+
+    def val(label):
+        got = [float(re.search(r"\[\s*([-\d.e+]+)", l).group(1)) for l in p.stdout.splitlines() if l.startswith(label)]
+        assert got, (label, p.stdout)
+        return got
+    x0 = val("a_global init:")[0]
+    assert -2.0 < x0 < 2.0  # Glorot-random start, like the notebook's -1.26032 / -1.17584
+    assert val("local a:") == [pytest.approx(0.1)]  # the local step leaves the global copy alone
+    assert val("a_global after worker 1 update:")[0] == pytest.approx(x0 + 0.1, abs=1e-6)
+    assert val("a_global seen by worker 2:")[0] == pytest.approx(x0 + 0.1, abs=1e-6)
+    after2 = val("a_global after worker 2 update:")
+    assert len(after2) == 2 and all(v == pytest.approx(x0 + 0.2, abs=1e-6) for v in after2)

@@ -141,6 +141,7 @@ def test_wgrad_side_stream_matches_main_stream(monkeypatch):
     g = torch.Generator(device="cpu").manual_seed(2)
     x0 = torch.randn(8, 64, 16, 16, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     gy, grads = None, []
+    was = overlap._ON
     try:
         for side in (False, True):
             overlap.set_enabled(side)
@@ -157,7 +158,7 @@ def test_wgrad_side_stream_matches_main_stream(monkeypatch):
             assert not overlap._pending  # joined by the end-of-backward callback
             grads.append([x.grad.float()] + [p.grad.float().clone() for p in bl.parameters()])
     finally:
-        overlap.set_enabled(False)
+        overlap.set_enabled(was)
     rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
     errs = [rel(ga, gb) for ga, gb in zip(grads[1], grads[0])]
     assert max(errs) < 1e-2, errs
@@ -202,3 +203,109 @@ def test_fused_stem_matches_unfused(flat, pairs, size, monkeypatch):
         assert a.shape == b.shape, name
         err = ((a - b).norm() / (a.norm() + 1e-6)).item()
         assert err < 2e-2, (name, err)
+
+
+def _ref_resnet_loss(model, params32, x32, y, drop_residual=None):
+    """Plain fp32 PyTorch ResNet (F.conv2d / F.batch_norm in training mode) over ``params32``: the
+    model's own weights as fp32 leaves.  ``drop_residual``: index of a block whose identity branch is
+    left out (the negative control)."""
+    import torch.nn.functional as F
+    P = params32
+
+    def cbn(x, pre, stride=1, pad=0, relu=True, res=None):
+        y = F.conv2d(x, P[pre + ".conv.weight"], None, stride, pad)
+        y = F.batch_norm(y, None, None, P[pre + ".bn.weight"], P[pre + ".bn.bias"], True, 0.0, 1e-5)
+        if res is not None:
+            y = y + res
+        return F.relu(y) if relu else y
+
+    h = cbn(x32, "stem", 2, 3)
+    h = F.max_pool2d(h, 3, 2, 1)
+    for i, blk in enumerate(model.blocks):
+        pre = "blocks.%d" % i
+        st = blk.c2.conv.stride
+        idn = cbn(h, pre + ".down", st, 0, relu=False) if blk.down is not None else h
+        t = cbn(h, pre + ".c1")
+        t = cbn(t, pre + ".c2", st, 1)
+        h = cbn(t, pre + ".c3", relu=True, res=None if i == drop_residual else idn)
+    h = h.mean(dim=(2, 3))
+    logits = F.linear(h, P["fc.weight"], P["fc.bias"])
+    return F.cross_entropy(logits, y)
+
+
+def test_resnet50_full_network_matches_fp32_reference():
+    """The whole fused ResNet-50 (stem node, 16 bottleneck nodes with the cross-block BN3 link, pools, FC,
+    softmax-xent) against an fp32 PyTorch model with identical weights: loss and EVERY parameter gradient.
+    A reference with one residual branch removed must fail the same bounds (the check can see a wiring
+    error)."""
+    from dtg.models.layers import BatchNorm2d
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = resnet.resnet50(100).to(dev).to(memory_format=torch.channels_last)
+    for m in model.modules():
+        if isinstance(m, BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)  # zero-init c3 gammas would hide every residual branch
+            m.bias.data.uniform_(-0.2, 0.2)
+    flat = FlatParams(model)
+    model.train()
+    x, y = resnet.synthetic_batch(8, dev, torch.bfloat16, 96, 100, seed=3)
+    loss = ops.softmax_cross_entropy(model(x), y)
+    loss.backward()
+    torch.cuda.synchronize()
+    names = [n for n, _ in model.named_parameters()]
+    got = {n: p.grad.float() for n, p in model.named_parameters()}
+
+    def reference(drop=None):
+        P = {n: p.detach().float().contiguous().clone().requires_grad_() for n, p in model.named_parameters()}
+        ref = _ref_resnet_loss(model, P, x.float(), y, drop_residual=drop)
+        ref.backward()
+        return ref.item(), {n: P[n].grad for n in names}
+
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    ref_loss, ref_g = reference()
+    errs = {n: rel(got[n], ref_g[n]) for n in names}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print("loss %.6f ref %.6f; worst grad rel-errs %s; median %.4f" % (
+        loss.item(), ref_loss, worst, sorted(errs.values())[len(errs) // 2]))
+    assert abs(loss.item() - ref_loss) < 2e-2 * abs(ref_loss)
+    assert sorted(errs.values())[len(errs) // 2] < 3e-2
+    assert max(errs.values()) < 1.5e-1, worst
+    _, bad_g = reference(drop=7)  # a block in layer3 without its identity branch
+    bad = sorted(rel(got[n], bad_g[n]) for n in names)
+    assert bad[-1] > 0.3 and bad[len(bad) // 2] > 3e-2, bad[-5:]
+
+
+def test_wgrad_side_stream_accumulates_into_existing_grad(monkeypatch):
+    """Parameters WITHOUT flat gradient buffers, two backward passes (the second adds into existing .grad,
+    as gradient accumulation does): the side-stream wgrads must be finished before autograd's
+    AccumulateGrad adds them on the main stream.  Side stream vs main stream must agree."""
+    from dtg.models.resnet import Bottleneck
+    from dtg.models import resnet_fused
+    from dtg.parallel import overlap
+    monkeypatch.setattr(resnet_fused, "_FUSE", True)
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x0 = torch.randn(16, 256, 28, 28, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    was = overlap._ON
+    try:
+        for side in (False, True):
+            overlap.set_enabled(side)
+            torch.manual_seed(0)
+            bl = torch.nn.Sequential(Bottleneck(256, 64, 1), Bottleneck(256, 128, 2)).to(dev)
+            bl = bl.to(memory_format=torch.channels_last)
+            for p in bl.parameters():
+                if p.dim() > 1:
+                    p.data = p.data.to(torch.bfloat16)
+            bl.train()
+            for it in range(2):
+                y = bl(x0.clone().requires_grad_())
+                gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(it)).to(dev, torch.bfloat16)
+                y.backward(gy.contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res.append([p.grad.float().clone() for p in bl.parameters()])
+    finally:
+        overlap.set_enabled(was)
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    errs = [rel(a, b) for a, b in zip(res[1], res[0])]
+    assert max(errs) < 1e-2, errs

@@ -24,13 +24,19 @@ run() {  # name timeout cmd...
 
 for s in "$@"; do
   case $s in
-    test) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    test) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     test_tf) run pytest_tf 600 python -m pytest tests/test_transformer_gpu.py -m gpu -q ;;
     bench_bert) run bench_bert 600 python bench.py --model bert --steps 20 --warmup 5 ;;
     prof_bert) run prof_bert 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bert -o run --output-format csv -- \
             python3 bench.py --model bert --steps 5 --warmup 3 ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_pg) DTG_DDP_FORCE=1 run bench_pg 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_pg_comm) DTG_DDP_FORCE=1 DTG_DDP_LAUNCH=comm run bench_pg_comm 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_pg_main) DTG_DDP_FORCE=1 DTG_WGRAD_STREAM=0 run bench_pg_main 600 python bench.py --steps 20 --warmup 5 ;;
+    prof_pg) DTG_DDP_FORCE=1 run prof_pg 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pg -o run --output-format csv -- \
+            python3 bench.py --steps 4 --warmup 3 ;;
+    test_resnet) run pytest_resnet 900 python -u -m pytest tests/test_resnet_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
     kbench) run kbench 600 python tools/bench_kernels.py --json gpurun_out/kbench.json ;;
     kbench_gemm_ab) DTG_GEMM_BIG=0 run kbench_small 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_small.json &&
