@@ -17,7 +17,8 @@ all-reduced per image (one model's gradients per step, whatever the batch).  Mea
 - ResNet-50: 10.5k img/s at 128, 12.1k at 256, 12.9k at 384, 13.4k at 512.
 - BERT-base: 6.2k seq/s at 64, 7.6k at 128, 8.2k at 256.
 
-``--model mnist`` measures BASELINE.json config 2 (MNIST CNN, per-GPU batch 512; a launch-bound step,
+``--mode async_ps --gpus N`` measures BASELINE.json config 4 (1 PS + N-1 ResNet-50 workers, RCCL
+point-to-point; see ``_async_ps``).  ``--model mnist`` measures BASELINE.json config 2 (MNIST CNN, per-GPU batch 512; a launch-bound step,
 so it replays as one hipGraph by default).  ``--batch`` overrides the default.  A timed step is the full training step: forward, fused softmax-xent,
 backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD apply.  W untimed
 warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
@@ -53,6 +54,10 @@ def parse(argv=None):
     # BERT, which are GPU-bound (>= 99 % kernel-busy): replay measured equal for ResNet-50 (11.93k vs
     # 11.97k img/s) and 2 % slower for BERT (profiles/r02_baselines)
     ap.add_argument("--graph", type=int, default=-1, help="-1 auto, 0 eager, 1 capture")
+    # BASELINE.json config 4: ResNet-50 asynchronous parameter server, rank 0 = PS, ranks 1..N-1 = workers
+    ap.add_argument("--mode", default="sync", choices=("sync", "async_ps"))
+    ap.add_argument("--window", type=int, default=1, help="async_ps: local steps per push (DOWNPOUR/ADAG window)")
+    ap.add_argument("--overlap_pull", type=int, default=1, help="async_ps: pull overlapped with the next step")
     return ap.parse_known_args(argv)[0]
 
 
@@ -113,11 +118,13 @@ def main(argv=None):
         return step
 
     rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
-    a.bucket_mb = a.bucket_mb or (25.0 if a.model == "bert" else 8.0)
     if world != a.gpus:
         # a mislabelled point on the scaling curve is worse than no point
         comm.shutdown()
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if a.mode == "async_ps":
+        return _async_ps(a, rank, world, device)
+    a.bucket_mb = a.bucket_mb or (25.0 if a.model == "bert" else 8.0)
     torch.manual_seed(1234)
     if device.type == "cuda":
         ops.lib()  # fail loudly if the HIP kernels are missing
@@ -218,6 +225,66 @@ def main(argv=None):
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init weights)", "config": config,
             "final_loss": final_loss}), flush=True)
+    comm.shutdown()
+
+
+def _async_ps(a, rank, world, device):
+    """BASELINE.json config 4: 1 PS + (N-1) ResNet-50 workers, Hogwild by default
+    (``--window T``: DOWNPOUR-style sum of T local gradients per push).  The PS rank owns a GPU and the
+    parameters; workers push gradients and pull parameters over RCCL point-to-point (parallel/async_ps.py).
+    Whole-node images/sec = PS-applied updates x images per update / wall time, counted on the PS from the
+    moment every worker has finished its W warm-up steps (a device synchronize on the PS brackets both
+    ends), so PS queueing and transfer stalls are inside the number.  Reference semantics: Hogwild/Hogwild.py:44-57,
+    DOWNPOUR/DOWNPOUR.py:96-102."""
+    import torch
+    from dtg import ops
+    from dtg.models import resnet
+    from dtg.optim import FusedSGD
+    from dtg.parallel import FlatParams, comm
+    from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
+    if world < 2:
+        comm.shutdown()
+        sys.exit("bench.py --mode async_ps needs --gpus >= 2 (one PS rank + workers)")
+    if device.type == "cuda":
+        from dtg import ops as _ops
+        _ops.lib()
+    a.batch = a.batch or 512
+    torch.manual_seed(1234)
+    model = resnet.resnet50().to(device).to(memory_format=torch.channels_last)
+    flat = FlatParams(model)
+    dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    if rank == 0:
+        opt = FusedSGD(flat, lr=a.lr or 0.1, momentum=0.9, weight_decay=5e-5)
+        ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, staleness_log=True)
+        ps.serve()
+        (u0, t0), (u1, t1) = ps.timed or ps.timed_end, ps.timed_end
+        imgs = (u1 - u0) * a.batch * a.window
+        ips = imgs / max(t1 - t0, 1e-9)
+        st = ps.staleness[u0:] or [0]
+        print(json.dumps({
+            "metric": "images/sec (whole node) ResNet-50 async PS, 1 PS + %d workers" % (world - 1),
+            "value": round(ips, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round((t1 - t0) / max(1, (u1 - u0) / (world - 1)) * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (random-init weights)",
+            "config": {"model": "ResNet-50", "per_gpu_batch": a.batch, "global_batch": a.batch * (world - 1),
+                       "image_size": a.image, "parallelism": "ps1+w%d" % (world - 1),
+                       "transport": "rccl p2p" if _backend_name() == "rccl" else _backend_name(),
+                       "window": a.window, "overlap_pull": bool(a.overlap_pull), "optimizer": "momentum-sgd (fused, on PS)"},
+            "updates_timed": u1 - u0, "per_worker": {str(k): v for k, v in ps.per_worker.items()},
+            "mean_staleness": round(sum(st) / len(st), 3), "lost_workers": ps.lost}), flush=True)
+        ps.close()
+    else:
+        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, overlap_pull=bool(a.overlap_pull))
+        x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
+        model.train()
+        w.begin()
+        for i in range(a.warmup + a.steps):
+            if i == a.warmup:
+                w.warm()
+            ops.softmax_cross_entropy(model(x), y).backward()
+            w.step_done()
+        w.finish()
     comm.shutdown()
 
 

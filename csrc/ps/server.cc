@@ -186,6 +186,13 @@ void Server::accept_loop() {
 
 void Server::serve(int fd) {
   std::vector<uint8_t> body;
+  // connection watch (failure detection): a client registers (queue, token); if its connection ends
+  // without UNWATCH -- the process died or dropped off the network -- the token is enqueued, so a
+  // consumer blocked on that queue learns about the loss instead of waiting out a timeout
+  bool watching = false;
+  std::string watch_q;
+  int64_t watch_tok = 0;
+  bool clean = false;
   while (!stopping_.load()) {
     ReqHdr h;
     if (!recv_all(fd, &h, sizeof(h))) break;
@@ -198,7 +205,15 @@ void Server::serve(int fd) {
     int32_t st = OK;
     try {
       Reader rd(body.data(), body.size());
-      st = dispatch(h.op, rd, wr);
+      if (h.op == WATCH) {
+        watch_q = rd.str();
+        watch_tok = rd.i64();
+        watching = true;
+      } else if (h.op == UNWATCH) {
+        watching = false;
+      } else {
+        st = dispatch(h.op, rd, wr);
+      }
     } catch (const std::exception& e) {
       st = ERR;
       wr.buf.clear();
@@ -208,9 +223,18 @@ void Server::serve(int fd) {
     if (!send_all(fd, &r, sizeof(r))) break;
     if (!wr.buf.empty() && !send_all(fd, wr.buf.data(), wr.buf.size())) break;
     bytes_out_ += (int64_t)(sizeof(r) + wr.buf.size());
-    if (h.op == SHUTDOWN) break;
+    if (h.op == SHUTDOWN) {
+      clean = true;
+      break;
+    }
   }
   ::shutdown(fd, SHUT_RDWR);
+  if (watching && !clean && !stopping_.load()) {
+    auto q = get_q(watch_q);
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->q.push_back(watch_tok);
+    q->cv.notify_all();
+  }
 }
 
 std::shared_ptr<Variable> Server::get_var(const std::string& name) {

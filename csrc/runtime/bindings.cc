@@ -271,6 +271,20 @@ class PyClient {
     call(wire::SHUTDOWN, w, &r);
   }
 
+  void watch(const std::string& queue, int64_t token) {
+    wire::Writer w;
+    w.str(queue);
+    w.i64(token);
+    std::vector<uint8_t> r;
+    call(wire::WATCH, w, &r);
+  }
+
+  void unwatch() {
+    wire::Writer w;
+    std::vector<uint8_t> r;
+    call(wire::UNWATCH, w, &r);
+  }
+
   int64_t heartbeat(int64_t task) {
     wire::Writer w;
     w.i64(task);
@@ -351,6 +365,8 @@ PYBIND11_MODULE(_runtime, m) {
       .def("worker_done", &PyClient::worker_done)
       .def("shutdown", &PyClient::shutdown)
       .def("heartbeat", &PyClient::heartbeat)
+      .def("watch", &PyClient::watch, py::arg("queue"), py::arg("token"))
+      .def("unwatch", &PyClient::unwatch)
       .def("stats", &PyClient::stats)
       .def("close", &PyClient::close);
 

@@ -4,6 +4,8 @@
 
 * ``kill_ps_at_step:N``  -- a PS task whose ``global_step`` variable reaches N dies abruptly
   (``os._exit(23)``, no clean shutdown: connections drop mid-request), once per process;
+* ``kill_rank_at_step:R@N`` -- rank R of a sync-DP job dies abruptly (``os._exit(23)``) when it is about to
+  run training step N (examples/ResNet50/resnet50_train.py; the survivors' watchdog or collective reports it);
 * ``drop_grad:P``        -- a worker silently drops each gradient push with probability P (a lost
   update; the async algorithms must tolerate it, sync ones need backup workers);
 * ``seed:S``             -- seed of the drop decisions (default 0).
@@ -36,6 +38,18 @@ def config():
 def kill_ps_step():
     v = _parse().get("kill_ps_at_step")
     return int(v) if v else None
+
+
+def maybe_kill_rank(rank, step):
+    """``kill_rank_at_step:R@N``: die like a crashed process if this is rank R about to run step N."""
+    v = _parse().get("kill_rank_at_step")
+    if not v:
+        return
+    r, _, n = v.partition("@")
+    if int(r) == int(rank) and int(n) == int(step):
+        import sys
+        print("dtg.fault: killing rank %d at step %d" % (rank, step), file=sys.stderr, flush=True)
+        os._exit(KILL_EXIT_CODE)
 
 
 _rng = None

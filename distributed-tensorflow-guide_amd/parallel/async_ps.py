@@ -16,20 +16,40 @@ workers intra-node (RCCL send/recv)").  Reference semantics kept:
   pulled (DynSGD, Jiang et al., SIGMOD 2017), so stale gradients from slow workers move the
   parameters less.
 
-MI355X design: parameters and optimizer state live in the PS GPU's flat buffers (FlatParams); a
-push is one RCCL send per dtype group (bf16 compute grads + fp32 norm/bias grads), a pull is one
-send of the bf16 compute mirror + fp32 group.  The PS serves all workers concurrently: it keeps
-one receive posted per worker (RCCL runs each PS<->worker pair on its own communicator/stream),
-applies whichever gradient lands first with the fused HIP optimizer kernel, snapshots the updated
-parameters into that worker's send buffer (so later applies cannot tear an in-flight send) and
-sends them back.
+MI355X design:
+
+* **payloads** go over RCCL point-to-point: torch's RCCL process group gives every PS<->worker pair its
+  own 2-rank communicator and HIP stream, so the 7 pairs of a node move gradients and parameters
+  concurrently, each over its own xGMI link.  A push is one send per dtype group (bf16 compute grads,
+  fp32 norm/bias grads, the BN running-statistics delta); a pull is the bf16 compute mirror, the fp32
+  group and the module buffers.
+* **request framing** goes over dtg's native TCP service (csrc/ps/server.cc, the same one the CPU PS
+  uses): a worker enqueues a (rank, kind) token on one queue and the PS blocks in ``q_dequeue`` with
+  the GIL released.  So the PS serves requests in arrival order with no busy spin and no device
+  synchronisation: its host loop only enqueues GPU work (post the receive, make the apply stream wait
+  for it, apply with the fused HIP optimizer kernel, snapshot, send), all ordered by streams and events.
+* **failure detection**: each worker's control connection carries a watch (``PSClient.watch``); if the
+  worker process dies, the service enqueues its "lost" token and ``serve()`` finishes with the
+  survivors (``lost`` lists who dropped out).  ``worker_timeout`` bounds how long the PS waits with no
+  request from any live worker (TimeoutError naming them).  A worker that dies in the middle of a
+  transfer leaves an RCCL kernel waiting on its pair stream; RCCL communicators cannot shrink, so that
+  case is fail-stop (the other workers' pulls stall and the PS times out), like sync DP.
+* **overlap** (``overlap_pull=True``): the worker snapshots its gradients into a send buffer, posts the
+  push and the pull, and goes on with its next step on the parameters it already has; the pulled ones
+  are swapped in (a device copy) at its next exchange.  That adds one step of staleness, which Hogwild
+  semantics allow, and takes the push -> PS apply -> pull round trip off the worker's critical path.
+  Without it the worker's GPU waits for the pull (its host does not).
 """
-import time
+import os
+import sys
 
 import torch
 import torch.distributed as dist
 
-_GRAD, _DONE, _ELASTIC = 1, 2, 3
+_GRAD, _DONE, _ELASTIC, _WARM = 1, 2, 3, 4
+_KINDS = 16
+_REQ = "dtg.aps.req"
+_instances = [0]  # per-process count of async-PS objects: the same on every rank (construction order)
 
 
 # gloo moves CPU tensors only for point-to-point; with DTG_BACKEND=gloo DTG_GLOO_DEVICE=cuda (the
@@ -39,20 +59,9 @@ def _staged(t, group):
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def _send(t, dst, group=None):
-    dist.send(t.cpu() if _staged(t, group) else t, dst=dst, group=group)
-
-
-def _recv(t, src=None, group=None):
-    if not _staged(t, group):
-        return dist.recv(t, src=src, group=group)
-    h = torch.empty_like(t, device="cpu")
-    peer = dist.recv(h, src=src, group=group)
-    t.copy_(h)
-    return peer
-
-
-from ..utils.trace import traced
+class _Done:
+    def wait(self):
+        pass
 
 
 class _HostSend:
@@ -66,12 +75,36 @@ class _HostSend:
         self._w.wait()
         self._h = None
 
-    def is_completed(self):
-        return self._w.is_completed()
+
+class _HostRecv:
+    """irecv into a host buffer; wait() lands it in the device tensor."""
+
+    def __init__(self, t, src, group):
+        self._t = t
+        self._h = torch.empty_like(t, device="cpu")
+        self._w = dist.irecv(self._h, src=src, group=group)
+
+    def wait(self):
+        self._w.wait()
+        self._t.copy_(self._h)
+        self._h = None
 
 
 def _isend(t, dst, group=None):
     return _HostSend(t, dst, group) if _staged(t, group) else dist.isend(t, dst=dst, group=group)
+
+
+def _irecv(t, src, group=None):
+    """Post a receive.  RCCL: ``wait()`` makes the CURRENT stream wait for it (no host block)."""
+    return _HostRecv(t, src, group) if _staged(t, group) else dist.irecv(t, src=src, group=group)
+
+
+def _wait_all(works):
+    for w in works:
+        w.wait()
+
+
+from ..utils.trace import traced  # noqa: E402
 
 
 def _group_payload_grads(flat):
@@ -93,39 +126,84 @@ def _elastic_state(flat):
     return [g.master for g in flat] + _buffers(flat)
 
 
+class _Control:
+    """Request framing between the PS rank and its workers over the native TCP service.  The PS hosts it
+    and publishes its address in the process group's store; workers connect and watch their connection."""
+
+    def __init__(self, is_ps, rank):
+        from .. import _runtime
+        _instances[0] += 1
+        key = "dtg.aps.ctl.%d" % _instances[0]
+        store = dist.distributed_c10d._get_default_store()
+        self.svc = None
+        if is_ps:
+            host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+            bind = "127.0.0.1" if host in ("127.0.0.1", "localhost") else "0.0.0.0"
+            self.svc = _runtime.PSServer(bind, 0, 0)
+            self.svc.start()
+            self.cli = _runtime.PSClient("127.0.0.1", self.svc.port, 60.0)
+            store.set(key, "%s:%d" % ("127.0.0.1" if bind == "127.0.0.1" else host, self.svc.port))
+        else:
+            addr = store.get(key).decode()
+            h, p = addr.rsplit(":", 1)
+            self.cli = _runtime.PSClient(h, int(p), 60.0)
+            self.cli.watch(_REQ, -(rank + 1))  # dies with the process -> the PS sees a lost token
+
+    def request(self, rank, kind):
+        self.cli.q_enqueue(_REQ, [rank * _KINDS + kind])
+
+    def next(self, timeout):
+        return self.cli.q_dequeue(_REQ, -1.0 if timeout is None else float(timeout))
+
+    def unwatch(self):
+        self.cli.unwatch()
+
+    def close(self):
+        if self.cli is not None:
+            self.cli.close()
+            self.cli = None
+        if self.svc is not None:
+            self.svc.stop()
+            self.svc = None
+
+
 class AsyncPSWorker:
     """Worker side.  ``begin()`` pulls the current parameters, ``step_done()`` after every backward
-    pushes/pulls every ``window`` steps, ``finish()`` tells the PS this worker is done (the PS's
-    ``serve()`` returns when all workers finished; a new begin()/serve() round may follow)."""
+    pushes/pulls every ``window`` steps, ``warm()`` marks the end of a warm-up phase (benchmarks),
+    ``finish()`` tells the PS this worker is done (the PS's ``serve()`` returns when all workers finished)."""
 
-    def __init__(self, flat, ps_rank=0, window=1, window_mode="sum", local_optimizer=None, group=None):
+    def __init__(self, flat, ps_rank=0, window=1, window_mode="sum", local_optimizer=None, group=None,
+                 overlap_pull=False):
         assert window_mode in ("sum", "mean")
         self.flat = flat
         self.ps = ps_rank
         self.pg = group
+        self.rank = dist.get_rank()
         self.window = max(1, int(window))
         self.window_mode = window_mode
         self.local_opt = local_optimizer
-        dev = next(iter(flat)).master.device
-        self.dev = dev
-        self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.overlap = bool(overlap_pull)
+        self._ctl = _Control(False, self.rank)
         self._acc = [torch.zeros_like(g.grad) for g in flat] if (self.window > 1 and local_optimizer) else None
         # module buffers as pulled: the push carries (current - pulled), the worker's running-statistics
         # update since the pull, which the PS adds to its own copy
         self._buf0 = [torch.empty_like(b) for b in _buffers(flat)]
         self._bufd = [torch.empty_like(b) for b in _buffers(flat)]
+        # overlap: gradient snapshot being sent, parameters being received (double buffers)
+        self._gsnap = [torch.empty_like(g.grad) for g in flat] if self.overlap else None
+        self._pbuf = [torch.empty_like(t) for t in _group_payload_params(flat)] if self.overlap else None
+        self._sends = []
+        self._pull = None
         self.local_step = 0
         self.pushes = 0
 
     def begin(self):
         """Initial pull (replaces the chief's assign_global + sleep(10) bootstrap,
         DOWNPOUR/DOWNPOUR.py:129-135)."""
-        self.pull()
+        _wait_all([_irecv(t, self.ps, self.pg) for t in _group_payload_params(self.flat)])
+        self._pulled()
 
-    @traced("dtg.ps.pull")
-    def pull(self):
-        for buf in _group_payload_params(self.flat):
-            _recv(buf, src=self.ps, group=self.pg)
+    def _pulled(self):
         for b0, b in zip(self._buf0, _buffers(self.flat)):
             b0.copy_(b)
         if self.local_opt is not None:
@@ -133,6 +211,17 @@ class AsyncPSWorker:
             for g in self.flat:
                 if g.mirror is not None:
                     g.master.copy_(g.mirror)
+
+    @traced("dtg.ps.pull")
+    def _land_pull(self):
+        """Overlap mode: the previous exchange's parameters -> the model (stream-ordered device copy)."""
+        if self._pull is None:
+            return
+        _wait_all(self._pull)
+        self._pull = None
+        for dst, src in zip(_group_payload_params(self.flat), self._pbuf):
+            dst.copy_(src)
+        self._pulled()
 
     @traced("dtg.ps.push")
     def step_done(self):
@@ -146,34 +235,52 @@ class AsyncPSWorker:
             self.local_opt.step()
         if self.local_step % self.window:
             return False
+        self._land_pull()
         grads = self._acc if self._acc is not None else _group_payload_grads(self.flat)
         for d, b, b0 in zip(self._bufd, _buffers(self.flat), self._buf0):
             torch.sub(b, b0, out=d)
-        self._hdr[0] = _GRAD
-        self._hdr[1] = self.local_step
-        _send(self._hdr, dst=self.ps, group=self.pg)
-        works = [_isend(t, dst=self.ps, group=self.pg) for t in list(grads) + self._bufd]
-        for w in works:
-            w.wait()
+        _wait_all(self._sends)  # the previous push's buffers are free again
+        if self.overlap:
+            for s, g in zip(self._gsnap, grads):
+                s.copy_(g)
+            grads_out = self._gsnap
+        else:
+            grads_out = grads
+        self._ctl.request(self.rank, _GRAD)
+        self._sends = [_isend(t, self.ps, self.pg) for t in list(grads_out) + self._bufd]
+        if self.overlap:
+            self._pull = [_irecv(t, self.ps, self.pg) for t in self._pbuf]
+        else:
+            _wait_all(self._sends)  # (stream-ordered) before the gradients are zeroed below
+            self._sends = []
         for t in grads:
             t.zero_()
         if self._acc is not None:
             self.flat.zero_grad()
-        self.pull()
+        if not self.overlap:
+            _wait_all([_irecv(t, self.ps, self.pg) for t in _group_payload_params(self.flat)])
+            self._pulled()
         self.pushes += 1
         return True
 
+    def warm(self):
+        """Tell the PS this worker has finished its warm-up (``AsyncPSServer.timed`` starts when all have)."""
+        self._ctl.request(self.rank, _WARM)
+
     def finish(self):
-        self._hdr[0] = _DONE
-        self._hdr[1] = self.local_step
-        _send(self._hdr, dst=self.ps, group=self.pg)
+        self._land_pull()
+        _wait_all(self._sends)
+        self._sends = []
+        self._ctl.unwatch()
+        self._ctl.request(self.rank, _DONE)
+        self._ctl.close()
 
 
 class AsyncPSServer:
-    """PS side: ``serve()`` runs until every worker sent DONE; returns the number of updates."""
+    """PS side: ``serve()`` runs until every worker sent DONE (or was lost); returns the number of updates."""
 
     def __init__(self, flat, optimizer, workers, window=1, window_mode="sum", group=None, staleness_log=False,
-                 staleness_scaling=None):
+                 staleness_scaling=None, worker_timeout=None):
         assert staleness_scaling in (None, "dyn")
         self.dyn = staleness_scaling == "dyn"
         self.flat = flat
@@ -181,12 +288,14 @@ class AsyncPSServer:
         self.workers = list(workers)
         self.pg = group
         self.gscale = 1.0 / window if window_mode == "mean" else 1.0
+        self.worker_timeout = worker_timeout if worker_timeout is not None else float(
+            os.environ.get("DTG_PS_WORKER_TIMEOUT", "600"))
         dev = next(iter(flat)).master.device
         self.dev = dev
+        self._ctl = _Control(True, dist.get_rank())
         self._recv = {w: [torch.empty_like(g.grad) for g in flat] for w in self.workers}
         self._recv_buf = {w: [torch.empty_like(b) for b in _buffers(flat)] for w in self.workers}
         self._snap = {w: [torch.empty_like(t) for t in _group_payload_params(flat)] for w in self.workers}
-        self._hdr = {w: torch.zeros(2, dtype=torch.int64, device=dev) for w in self.workers}
         self._send_works = {w: [] for w in self.workers}
         self.updates = 0
         self.version = 0
@@ -194,14 +303,16 @@ class AsyncPSServer:
         self.staleness = [] if staleness_log else None
         self.scales = [] if staleness_log else None
         self.per_worker = {w: 0 for w in self.workers}
+        self.lost = []
+        self._warm = set()
+        self.timed = None  # (updates, time) when every worker reported warm; serve() fills timed_end
 
     def _send_params(self, w):
-        for prev in self._send_works[w]:
-            prev.wait()  # the snapshot buffer is about to be overwritten
+        _wait_all(self._send_works[w])  # the snapshot buffer is about to be overwritten (stream wait)
         snap = self._snap[w]
         for s, p in zip(snap, _group_payload_params(self.flat)):
             s.copy_(p)
-        self._send_works[w] = [_isend(s, dst=w, group=self.pg) for s in snap]
+        self._send_works[w] = [_isend(s, w, self.pg) for s in snap]
         self._pulled_version[w] = self.version
 
     @traced("dtg.ps.apply")
@@ -228,38 +339,29 @@ class AsyncPSServer:
         self.updates += 1
         self.per_worker[w] += 1
 
-    def _handle(self, w):
-        """Header from worker w has landed: DONE -> False; else receive, apply, reply -> True."""
-        kind = int(self._hdr[w][0].item())
-        if kind == _DONE:
-            return False
-        if kind == _ELASTIC:
-            self._elastic(w)
-            return True
-        for b in self._recv[w] + self._recv_buf[w]:
-            _recv(b, src=w, group=self.pg)
+    def _grad(self, w):
+        # the receive is posted from the apply (current) stream, so RCCL's pair stream first waits for the
+        # previous apply that read these buffers; the apply then waits for the receive (stream events only)
+        _wait_all([_irecv(b, w, self.pg) for b in self._recv[w] + self._recv_buf[w]])
         self._apply(w)
         self._send_params(w)
-        return True
 
     def _elastic(self, w):
         """EASGD exchange (Zhang, Choromanska, LeCun 2015): receive the worker's parameters x_i,
         d = alpha * (x_i - x~), x~ += d, send d back (the worker applies x_i -= d)."""
         bufs = self._recv_elastic[w]
-        for b in bufs:
-            _recv(b, src=w, group=self.pg)
+        _wait_all([_irecv(b, w, self.pg) for b in bufs])
         with torch.no_grad():
             for c, b in zip(_elastic_state(self.flat), bufs):
                 b.sub_(c).mul_(self.elastic_alpha)
                 c.add_(b)
             for g in self.flat:
                 g.refresh_mirror()
-        for prev in self._send_works[w]:
-            prev.wait()
+        _wait_all(self._send_works[w])
         snap = self._snap_elastic[w]
         for s_, b in zip(snap, bufs):
             s_.copy_(b)
-        self._send_works[w] = [_isend(s_, dst=w, group=self.pg) for s_ in snap]
+        self._send_works[w] = [_isend(s_, w, self.pg) for s_ in snap]
         self.version += 1
         self.updates += 1
         self.per_worker[w] += 1
@@ -271,45 +373,52 @@ class AsyncPSServer:
         self._snap_elastic = {w: [torch.empty_like(t) for t in _elastic_state(self.flat)] for w in self.workers}
         return self
 
-    def serve(self, poll_sleep=0.0):
+    def _sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def serve(self, poll_sleep=None):
+        """Serve requests in arrival order until every worker is done or lost.  (``poll_sleep`` is
+        accepted for compatibility; the loop blocks in the native queue and never polls.)"""
+        import time
+        live = set(self.workers)
         for w in self.workers:
             self._send_params(w)
-        if dist.get_backend(self.pg) == "gloo":
-            self._serve_any_source()
-        else:
-            self._serve_polling(poll_sleep)
+        while live:
+            tok = self._ctl.next(self.worker_timeout)
+            if tok is None:
+                raise TimeoutError("async PS: no request from workers %s in %.0f s" % (sorted(live),
+                                                                                       self.worker_timeout))
+            if tok < 0:
+                w = -tok - 1
+                if w in live:
+                    live.discard(w)
+                    self.lost.append(w)
+                    print("[dtg.async_ps] worker rank %d lost (its control connection closed); continuing with %s"
+                          % (w, sorted(live)), file=sys.stderr, flush=True)
+                continue
+            w, kind = divmod(tok, _KINDS)
+            if kind == _DONE:
+                live.discard(w)
+            elif kind == _WARM:
+                self._warm.add(w)
+                if self._warm >= set(self.workers) - set(self.lost) and self.timed is None:
+                    self._sync()
+                    self.timed = (self.updates, time.perf_counter())
+            elif kind == _ELASTIC:
+                self._elastic(w)
+            else:
+                self._grad(w)
         for w in self.workers:
-            for s in self._send_works[w]:
-                s.wait()
+            if w not in self.lost:
+                _wait_all(self._send_works[w])
+            self._send_works[w] = []
+        self._sync()
+        self.timed_end = (self.updates, time.perf_counter())
         return self.updates
 
-    def _serve_polling(self, poll_sleep):
-        # RCCL: one header receive posted per worker (each on its pair communicator); serve
-        # whichever completes first
-        pending = {w: dist.irecv(self._hdr[w], src=w, group=self.pg) for w in self.workers}
-        while pending:
-            progressed = False
-            for w in list(pending):
-                if not pending[w].is_completed():
-                    continue
-                pending[w].wait()
-                progressed = True
-                if self._handle(w):
-                    pending[w] = dist.irecv(self._hdr[w], src=w, group=self.pg)
-                else:
-                    del pending[w]
-            if not progressed and poll_sleep:
-                time.sleep(poll_sleep)
-
-    def _serve_any_source(self):
-        # gloo: receive-from-any-source gives arrival order directly
-        live = set(self.workers)
-        hdr = torch.zeros(2, dtype=torch.int64, device=self.dev)
-        while live:
-            w = _recv(hdr, group=self.pg)  # returns the sender's global rank
-            self._hdr[w].copy_(hdr)
-            if not self._handle(w):
-                live.discard(w)
+    def close(self):
+        self._ctl.close()
 
 
 class ElasticWorker:
@@ -327,16 +436,15 @@ class ElasticWorker:
         self.tau = max(1, int(tau))
         self.ps = ps_rank
         self.pg = group
-        dev = next(iter(flat)).master.device
-        self._hdr = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.rank = dist.get_rank()
+        self._ctl = _Control(False, self.rank)
         self._d = [torch.empty_like(t) for t in _elastic_state(flat)]
         self.local_step = 0
         self.exchanges = 0
 
     def begin(self):
         """Start from the center: receive the PS parameters (mirror / fp32 group) into the replica."""
-        for buf in _group_payload_params(self.flat):
-            _recv(buf, src=self.ps, group=self.pg)
+        _wait_all([_irecv(t, self.ps, self.pg) for t in _group_payload_params(self.flat)])
         with torch.no_grad():
             for g in self.flat:
                 if g.mirror is not None:
@@ -348,14 +456,9 @@ class ElasticWorker:
         self.opt.step()
         if self.local_step % self.tau:
             return False
-        self._hdr[0] = _ELASTIC
-        self._hdr[1] = self.local_step
-        _send(self._hdr, dst=self.ps, group=self.pg)
-        works = [_isend(t, dst=self.ps, group=self.pg) for t in _elastic_state(self.flat)]
-        for w in works:
-            w.wait()
-        for d in self._d:
-            _recv(d, src=self.ps, group=self.pg)
+        self._ctl.request(self.rank, _ELASTIC)
+        _wait_all([_isend(t, self.ps, self.pg) for t in _elastic_state(self.flat)])
+        _wait_all([_irecv(d, self.ps, self.pg) for d in self._d])
         with torch.no_grad():
             for t, d in zip(_elastic_state(self.flat), self._d):
                 t.sub_(d)
@@ -365,9 +468,9 @@ class ElasticWorker:
         return True
 
     def finish(self):
-        self._hdr[0] = _DONE
-        self._hdr[1] = self.local_step
-        _send(self._hdr, dst=self.ps, group=self.pg)
+        self._ctl.unwatch()
+        self._ctl.request(self.rank, _DONE)
+        self._ctl.close()
 
 
 def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1):

@@ -21,24 +21,25 @@ independent kernels instead of one.
 * a gradient all-reduce launched during backward (parallel/ddp.py) first makes the main stream wait
   for the side stream (an event, no host sync), then is enqueued from the main stream as usual.
 
-Several ranks: the main stream only, by default.  The opt-in form (``DTG_WGRAD_STREAM=2``) enqueues a
-bucket's collective from a third stream that waits for both the main and the side stream
-(parallel/ddp.py), so neither stalls.  That needs at least 8 hardware queues per process
-(``GPU_MAX_HW_QUEUES=8``): with HIP's default of 4, the main, side, collective and RCCL streams share
-hardware queues and their kernels serialise.  A one-rank RCCL process group (``DTG_DDP_FORCE=1``) on one
-GPU shows it (ResNet-50 b512, profiles/r02_side_stream_ddp):
+Several ranks over RCCL: the side stream is used too, and a bucket's collective is enqueued from it
+(parallel/ddp.py).  What decides the speed is which HIP streams share a hardware queue: a HIP process
+gets GPU_MAX_HW_QUEUES=4 queues by default, streams are bound to queues when torch creates its stream
+pools, and two streams on one queue serialise (a cross-stream wait packet blocks the whole queue).  A
+rocprofv3 kernel trace (Queue_Id per dispatch) of a one-rank RCCL group (``DTG_DDP_FORCE=1``, ResNet-50
+b512; profiles/r03_streams) showed the side stream drawn from torch's pool onto the main stream's queue
+once the process group had taken its own pool stream first.  Queues are per priority, so the side stream
+is a HIGH-priority stream (its own queue, never the main stream's) and the process group's collective
+stream is high-priority too (parallel/comm.py):
 
-- main stream only: 13.96k img/s;
-- side stream at 4 queues: 12.37k;
-- side stream at 8 queues: 14.48k (no process group at all: 14.58k).
+- main stream only: 13.86k img/s;  side stream, normal priority: 12.37k (main and side on one queue);
+- side high-priority, process group normal: 13.97k;  both high-priority: 14.47k;
+- both normal but GPU_MAX_HW_QUEUES=8: 14.50k;  no process group at all: 14.58k.
 
-It stays opt-in because the one-GPU-per-rank RCCL case cannot be run from here, and 8 queues per process
-hung the two-rank gloo rehearsal, where both ranks share one card.  gloo (host-staged) always keeps the
-wgrads on the main stream: there the side stream ran 9-40x slower (profiles/r02_overlap), because the
-staging copies synchronise the host.
+gloo (host-staged) keeps the wgrads on the main stream: there the side stream ran 9-40x slower
+(profiles/r02_overlap), because the staging copies synchronise the host.
 
 ``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).  ``=2`` forces the side stream
-with several ranks, whatever the backend and queue count.  Measured gain on one rank:
+with several gloo ranks too.  ``DTG_SIDE_PRIO=0`` gives the side stream normal priority.  Measured gain on one rank:
 ResNet-50 +2.3 % (+4 % with the side-stream split targets of models/resnet_fused.py), BERT-base +1.1 %.
 The record_stream version once ran a whole bench 5x slower (191 ms/step instead of 37 ms, same losses),
 most likely because its allocator reserve kept growing (profiles/r02_overlap).
@@ -50,6 +51,7 @@ import torch
 
 _ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
 _MULTI = os.environ.get("DTG_WGRAD_STREAM") == "2"  # also with several ranks (rehearsals)
+_PRIO = int(os.environ.get("DTG_SIDE_PRIO", "-1"))  # torch stream priority of the side stream (-1: high)
 _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()
@@ -77,7 +79,7 @@ def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        s = _side[idx] = torch.cuda.Stream(device=idx)
+        s = _side[idx] = torch.cuda.Stream(device=idx, priority=_PRIO)
     return s
 
 

@@ -235,6 +235,8 @@ class Saver:
 
 
 # ---- flat-buffer models ---------------------------------------------------------------------
+SLOT_LAYOUT_KEY = "dtg/slot_layout"
+SLOT_LAYOUT_LOGICAL = 1
 def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_dir=None, optimizer=None):
     """Checkpoint a FlatParams model (+ module buffers, optimizer state) as a TensorBundle."""
     arrays = [(n, _np_of(v)) for n, v in flat.named_masters()]
@@ -242,6 +244,10 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
         arrays.append((n, _np_of(b)))
     if optimizer is not None:
         from ..parallel.flat import _view_like
+        # slots are stored in LOGICAL parameter order (round 3); older checkpoints held channels_last conv
+        # slots in physical [K,R,S,C] order under the same keys -- restore_flat converts those
+        arrays.append((SLOT_LAYOUT_KEY, np.array(SLOT_LAYOUT_LOGICAL, dtype=np.int64)))
+        arrays.append(("optimizer/step", np.array(int(getattr(optimizer, "step_count", 0)), dtype=np.int64)))
         for g in flat:
             for k, buf in g.state.items():
                 for i, n in enumerate(g.names):
@@ -269,20 +275,38 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
 
 
 def restore_flat(flat, prefix, optimizer=None):
+    """Restore what :func:`save_flat` wrote.  With ``optimizer``: its slots too (created when the optimizer
+    has not stepped yet) and its step count.  Returns the checkpoint's global step (or None)."""
     from ..parallel.flat import _view_like
     vals = read_tensors(prefix)
+    logical = int(vals.get(SLOT_LAYOUT_KEY, -1)) == SLOT_LAYOUT_LOGICAL
     with torch.no_grad():
         for g in flat:
+            if optimizer is not None:  # slots present in the checkpoint but not yet allocated
+                for n in g.names:
+                    for key in vals:
+                        if key.startswith(n + "/") and "/" not in key[len(n) + 1:]:
+                            g.state_buffer(key[len(n) + 1:])
             for i, n in enumerate(g.names):
                 mv = g.master_view(i)
                 mv.copy_(torch.from_numpy(vals[n]).view(mv.shape))
                 for k, buf in g.state.items():
                     key = "%s/%s" % (n, k)
                     if key in vals:
-                        sv = _view_like(buf, g.offsets[i], g.params[i])
-                        sv.copy_(torch.from_numpy(vals[key]).view(sv.shape))
+                        p = g.params[i]
+                        sv = _view_like(buf, g.offsets[i], p)
+                        src = torch.from_numpy(vals[key])
+                        if not logical and p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(
+                                memory_format=torch.channels_last):
+                            o, c, r, s_ = p.shape  # legacy physical [K,R,S,C] slot order
+                            src = src.reshape(o, r, s_, c).permute(0, 3, 1, 2)
+                        sv.copy_(src.reshape(sv.shape))
             g.refresh_mirror()
         for n, b in flat.module.named_buffers():
             if n in vals:
                 b.copy_(torch.from_numpy(vals[n]).view(b.shape))
+    if optimizer is not None and "optimizer/step" in vals and hasattr(optimizer, "step_count"):
+        optimizer.step_count = int(vals["optimizer/step"])
+        if hasattr(optimizer, "hyper"):
+            optimizer.hyper[1].fill_(float(optimizer.step_count))
     return int(vals["global_step"]) if "global_step" in vals else None

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--window_mode", default="sum", choices=("sum", "mean"))
     ap.add_argument("--dyn_sgd", action="store_true",
                     help="Dynamic SGD: scale each PS update by 1/(staleness+1) (reference README TODO)")
+    ap.add_argument("--overlap_pull", action="store_true",
+                    help="pull overlapped with the next step (one extra step of staleness, Hogwild allows it)")
     ap.add_argument("--tiny", action="store_true", help="narrow 4-block ResNet, 32x32 images (CPU smoke tests)")
     a, _ = ap.parse_known_args()
     cluster = {"ps": [f"localhost:{a.base_port}"],
@@ -57,7 +59,7 @@ def main():
         print(f"[ps] {n} updates in {dt:.1f}s, per worker {ps.per_worker}, mean staleness "
               f"{sum(st) / max(1, len(st)):.2f}", flush=True)
     else:
-        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode)
+        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode, overlap_pull=a.overlap_pull)
         dt_ = torch.bfloat16 if device.type == "cuda" else torch.float32
         x, y = resnet.synthetic_batch(a.batch, device, dt_, a.image, ncls, seed=rank)
         w.begin()

@@ -281,3 +281,119 @@ def test_async_ps_carries_bn_running_stats():
     ps = {n: torch.as_tensor(v) for n, v in out[0]["bufs"].items()}
     assert ps["n.running_mean"].abs().max() > 1e-3
     assert (ps["n.running_var"] - 1).abs().max() > 1e-3
+
+
+def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeout=None, stall=None):
+    """Hogwild ranks with the worker-side options: overlapped pulls, a worker that dies (os._exit, no
+    finish) after ``die_after`` steps, a PS ``worker_timeout`` with a worker that stalls."""
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import time
+        import dtg  # noqa: F401
+        from dtg import ops
+        from dtg.optim import FusedSGD
+        from dtg.parallel import FlatParams, comm
+        from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
+        comm.init("gloo")
+        model = _model()
+        flat = FlatParams(model, compute_dtype=torch.float32)
+        if rank == 0:
+            ps = AsyncPSServer(flat, FusedSGD(flat, lr=0.1, momentum=0.0), workers=range(1, world),
+                               staleness_log=True, worker_timeout=timeout)
+            try:
+                n = ps.serve()
+            except TimeoutError as e:
+                q.put((rank, "ok", {"timeout": str(e)}))
+                q.close()
+                q.join_thread()  # flush before the hard exit
+                os._exit(0)
+            q.put((rank, "ok", {"updates": n, "per_worker": dict(ps.per_worker), "lost": list(ps.lost),
+                                "w": [g.master.clone().numpy() for g in flat], "staleness": list(ps.staleness)}))
+        else:
+            w = AsyncPSWorker(flat, ps_rank=0, overlap_pull=overlap)
+            w.begin()
+            x, y = _data(rank)
+            for i in range(steps):
+                loss = ops.softmax_cross_entropy(model(x), y)
+                loss.backward()
+                w.step_done()
+                if die_after is not None and rank == world - 1 and i + 1 == die_after:
+                    q.put((rank, "ok", {"died": True}))
+                    q.close()
+                    q.join_thread()
+                    os._exit(3)  # no finish(), no shutdown: the process just disappears
+                if stall is not None and rank == world - 1 and i + 1 == stall:
+                    q.put((rank, "ok", {"stalled": True}))
+                    q.close()
+                    q.join_thread()
+                    time.sleep(60)
+                    os._exit(0)
+            w.finish()
+            q.put((rank, "ok", {"pushes": w.pushes}))
+        comm.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+        raise
+
+
+def _run_opts(world, steps, **kw):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_opts, args=(r, world, port, steps, q), kwargs=kw) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, status, payload = q.get(timeout=240)
+        assert status == "ok", status
+        out[r] = payload
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    return out
+
+
+def test_async_ps_overlapped_pull_equals_lagged_replay():
+    """overlap_pull: the worker's step t gradient is computed on the PS parameters after update t-2 (one
+    extra step of staleness, the pull lands at the next exchange); with one worker that is deterministic."""
+    steps = 10
+    out = _run_opts(2, steps, overlap=True)
+    assert out[0]["updates"] == steps and out[1]["pushes"] == steps
+    import dtg  # noqa: F401
+    from dtg import ops
+    model = _model()
+    x, y = _data(1)
+    params = list(model.parameters())
+    hist = [[p.detach().clone() for p in params]]  # PS states P_0, P_1, ...
+    for t in range(1, steps + 1):
+        used = hist[max(0, t - 2)]
+        with torch.no_grad():
+            for p, v in zip(params, used):
+                p.copy_(v)
+        loss = ops.softmax_cross_entropy(model(x), y)
+        grads = torch.autograd.grad(loss, params)
+        hist.append([h - 0.1 * g for h, g in zip(hist[-1], grads)])
+    got = _ps_params_by_name(out)
+    for (n, _), v in zip(model.named_parameters(), hist[-1]):
+        assert torch.allclose(got[n], v, atol=1e-5), n
+
+
+def test_async_ps_survives_a_dead_worker():
+    """A worker process that vanishes mid-run (SURVEY §4.2 fault injection): its control connection drops,
+    the PS drops it and finishes with the survivor, every update it did push counted once."""
+    out = _run_opts(3, 12, die_after=4)
+    assert out[2] == {"died": True}
+    assert out[0]["lost"] == [2]
+    assert out[0]["per_worker"] == {1: 12, 2: 4} and out[0]["updates"] == 16
+
+
+def test_async_ps_worker_timeout_names_silent_workers():
+    out = _run_opts(2, 6, timeout=3.0, stall=2)
+    assert "no request from workers [1]" in out[0]["timeout"]

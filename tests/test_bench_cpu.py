@@ -43,3 +43,16 @@ def test_world_size_mismatch_is_an_error():
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
     assert not any(x.startswith("{") for x in r.stdout.splitlines())
+
+
+def test_async_ps_mode_reports_whole_node_rate():
+    """bench.py --mode async_ps (BASELINE config 4): rank 0 is the PS, the other ranks are workers; the PS
+    prints one JSON line of whole-node images/sec over the updates applied after every worker's warm-up."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--mode", "async_ps",
+                        "--batch", "2", "--image", "32", "--steps", "3", "--warmup", "1"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    j = _json_line(r.stdout)
+    assert j["n_gpus"] == 3 and j["config"]["parallelism"] == "ps1+w2" and j["value"] > 0
+    assert j["per_worker"] == {"1": 4, "2": 4} and j["lost_workers"] == []
+    assert 1 <= j["updates_timed"] <= 8

@@ -236,43 +236,56 @@ def _ref_resnet_loss(model, params32, x32, y, drop_residual=None):
 def test_resnet50_full_network_matches_fp32_reference():
     """The whole fused ResNet-50 (stem node, 16 bottleneck nodes with the cross-block BN3 link, pools, FC,
     softmax-xent) against an fp32 PyTorch model with identical weights: loss and EVERY parameter gradient.
-    A reference with one residual branch removed must fail the same bounds (the check can see a wiring
-    error)."""
+
+    A 50-layer ReLU network's gradients are sensitive to bf16-sized perturbations at any init (ReLU masks
+    flip): the fp32 reference itself moves by ~27 % (median per-tensor) when its weights get 2^-9 relative
+    noise (tools/resnet_numerics_diag.py).  So the bound is relative to that noise floor, measured in the
+    test, and a wiring error must stand far above it: a reference with one residual branch removed has to
+    disagree much more than dtg does."""
     from dtg.models.layers import BatchNorm2d
     torch.manual_seed(0)
     dev = torch.device("cuda")
     model = resnet.resnet50(100).to(dev).to(memory_format=torch.channels_last)
-    for m in model.modules():
-        if isinstance(m, BatchNorm2d):
-            m.weight.data.uniform_(0.5, 1.5)  # zero-init c3 gammas would hide every residual branch
+    for name, m in model.named_modules():
+        if isinstance(m, BatchNorm2d):  # zero-init c3 gammas would hide every residual branch
+            m.weight.data.uniform_(*((0.1, 0.3) if name.endswith("c3.bn") else (0.8, 1.2)))
             m.bias.data.uniform_(-0.2, 0.2)
-    flat = FlatParams(model)
+    FlatParams(model)
     model.train()
-    x, y = resnet.synthetic_batch(8, dev, torch.bfloat16, 96, 100, seed=3)
+    x, y = resnet.synthetic_batch(16, dev, torch.bfloat16, 64, 100, seed=3)
     loss = ops.softmax_cross_entropy(model(x), y)
     loss.backward()
     torch.cuda.synchronize()
     names = [n for n, _ in model.named_parameters()]
     got = {n: p.grad.float() for n, p in model.named_parameters()}
 
-    def reference(drop=None):
-        P = {n: p.detach().float().contiguous().clone().requires_grad_() for n, p in model.named_parameters()}
+    def reference(drop=None, noise=0.0):
+        g = torch.Generator(device="cpu").manual_seed(11)
+        P = {}
+        for n, p in model.named_parameters():
+            t = p.detach().float().contiguous().clone()
+            if noise:
+                t = t * (1 + noise * torch.randn(t.shape, generator=g).to(dev))
+            P[n] = t.requires_grad_()
         ref = _ref_resnet_loss(model, P, x.float(), y, drop_residual=drop)
         ref.backward()
         return ref.item(), {n: P[n].grad for n in names}
 
     rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     ref_loss, ref_g = reference()
-    errs = {n: rel(got[n], ref_g[n]) for n in names}
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    print("loss %.6f ref %.6f; worst grad rel-errs %s; median %.4f" % (
-        loss.item(), ref_loss, worst, sorted(errs.values())[len(errs) // 2]))
-    assert abs(loss.item() - ref_loss) < 2e-2 * abs(ref_loss)
-    assert sorted(errs.values())[len(errs) // 2] < 3e-2
-    assert max(errs.values()) < 1.5e-1, worst
-    _, bad_g = reference(drop=7)  # a block in layer3 without its identity branch
-    bad = sorted(rel(got[n], bad_g[n]) for n in names)
-    assert bad[-1] > 0.3 and bad[len(bad) // 2] > 3e-2, bad[-5:]
+    _, noisy_g = reference(noise=2 ** -9)
+    _, bad_g = reference(drop=7)  # a layer3 block without its identity branch
+    e_dtg = {n: rel(got[n], ref_g[n]) for n in names}
+    e_noise = med([rel(noisy_g[n], ref_g[n]) for n in names])
+    e_bad = med([rel(got[n], bad_g[n]) for n in names])
+    print("loss %.6f ref %.6f | median grad rel-err: dtg %.4f, fp32 ref under 2^-9 weight noise %.4f, "
+          "dtg vs ref without one residual %.4f" % (loss.item(), ref_loss, med(e_dtg.values()), e_noise, e_bad))
+    assert abs(loss.item() - ref_loss) < 2e-3 * abs(ref_loss)
+    assert e_dtg["fc.weight"] < 2e-2 and e_dtg["fc.bias"] < 2e-2  # the last layer sees no chaos
+    assert med(e_dtg.values()) < 1.6 * e_noise + 0.02
+    assert max(e_dtg.values()) < 0.7, sorted(e_dtg.items(), key=lambda kv: -kv[1])[:5]
+    assert e_bad > 2.0 * med(e_dtg.values())
 
 
 def test_wgrad_side_stream_accumulates_into_existing_grad(monkeypatch):
