@@ -41,9 +41,9 @@ enum Op : uint16_t {
   ACC_NUM = 18,      // name -> i64 num accumulated
   STATS = 19,        // -> i64 requests, i64 bytes_in, i64 bytes_out, i64 applies
   HEARTBEAT = 20,    // i64 task -> i64 server time ms
-  WATCH = 21,        // name, i64 token: if THIS connection closes before UNWATCH, enqueue token on queue name
-  UNWATCH = 22,      // clears this connection's watch
   Q_SIZE = 21,       // name -> i64
+  WATCH = 40,        // name, i64 token: if THIS connection closes before UNWATCH, enqueue token on queue name
+  UNWATCH = 41,      // clears this connection's watch
 };
 
 enum DType : uint8_t { F32 = 1, F64 = 2, I32 = 3, I64 = 9, BF16 = 14 };
