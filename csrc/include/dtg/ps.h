@@ -111,6 +111,7 @@ class Server {
   bool shutdown_ = false;
 
   std::atomic<int64_t> n_requests_{0}, bytes_in_{0}, bytes_out_{0}, n_applies_{0};
+  int64_t n_lost_ = 0;  // worker tasks whose watched connection dropped before they reported done
 };
 
 class Client {

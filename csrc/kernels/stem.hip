@@ -386,9 +386,17 @@ __global__ void __launch_bounds__(256) stem_bwd_band_kernel(const bf16_t* __rest
   }
 }
 
-static bool stem_band_ok(int H, int C, int k, int s, int pad, int P) {
+// dynamic LDS of the banded backward (see stem_bn_pool_bwd); must fit one workgroup's LDS (160 KB on gfx950),
+// larger images (wide rows) take the per-pixel gather form instead
+static size_t stem_band_lds(int Q, int C) {
+  const size_t a = (size_t)3 * Q * C * 3, b = (size_t)2 * 32 * C * 4;
+  return a > b ? a : b;
+}
+
+static bool stem_band_ok(int H, int C, int k, int s, int pad, int P, int Q) {
   static const bool on = !getenv("DTG_STEM_BAND") || atoi(getenv("DTG_STEM_BAND")) != 0;
-  return on && k == 3 && s == 2 && pad == 1 && C == 64 && H % kStemBandRows == 0 && P == (H - 1) / 2 + 1;
+  return on && k == 3 && s == 2 && pad == 1 && C == 64 && H % kStemBandRows == 0 && P == (H - 1) / 2 + 1 &&
+         stem_band_lds(Q, C) <= (size_t)160 * 1024;
 }
 
 // ---- input packing for the pixel-pair stem conv (ops/conv.py stem_pairs) ---------------------------
@@ -481,8 +489,8 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   float* part = ws;
   float* coef = ws + (long long)bg.nchunk * 2 * C;
-  if (stem_band_ok(H, C, k, s, pad, P) && bg.nchunk >= kBnStatSlots) {
-    const size_t lds = (size_t)3 * Q * C * 3 > (size_t)2 * 32 * C * 4 ? (size_t)3 * Q * C * 3 : (size_t)2 * 32 * C * 4;
+  if (stem_band_ok(H, C, k, s, pad, P, Q) && bg.nchunk >= kBnStatSlots) {
+    const size_t lds = stem_band_lds(Q, C);
     const unsigned nb = (unsigned)(N * (H / kStemBandRows));
     DTG_HIP_CHECK(hipMemsetAsync(part, 0, (size_t)kBnStatSlots * 2 * C * sizeof(float), st));
     hipLaunchKernelGGL(stem_bwd_band_kernel<false>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
@@ -492,6 +500,7 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
                                                            const_cast<float*>(sinv), 0.f, 0.f, coef, dgamma, dbeta);
     hipLaunchKernelGGL(stem_bwd_band_kernel<true>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
                        sinv, coef, g, nullptr, dy);
+    DTG_HIP_CHECK(hipGetLastError());  // a failed launch must not leave dy / the partials as garbage
     return;
   }
   dim3 grid(bg.nchunk, bg.gy);

@@ -229,7 +229,16 @@ void Server::serve(int fd) {
     }
   }
   ::shutdown(fd, SHUT_RDWR);
-  if (watching && !clean && !stopping_.load()) {
+  if (watching && !clean && !stopping_.load() && watch_q == "__worker__") {
+    // a worker task's process is gone: count it as finished so join() does not wait for it forever
+    std::lock_guard<std::mutex> lk(done_mu_);
+    if (watch_tok >= 0 && watch_tok < (int64_t)worker_done_.size() && !worker_done_[watch_tok]) {
+      worker_done_[watch_tok] = true;
+      done_count_++;
+      n_lost_++;
+    }
+    done_cv_.notify_all();
+  } else if (watching && !clean && !stopping_.load()) {
     auto q = get_q(watch_q);
     std::lock_guard<std::mutex> lk(q->mu);
     q->q.push_back(watch_tok);
@@ -673,7 +682,13 @@ void Server::stop() {
 }
 
 std::map<std::string, int64_t> Server::stats() {
+  int64_t lost;
+  {
+    std::lock_guard<std::mutex> lk(done_mu_);
+    lost = n_lost_;
+  }
   return {{"requests", n_requests_.load()},
+          {"workers_lost", lost},
           {"bytes_in", bytes_in_.load()},
           {"bytes_out", bytes_out_.load()},
           {"applies", n_applies_.load()}};

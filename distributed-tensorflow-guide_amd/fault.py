@@ -6,6 +6,8 @@
   (``os._exit(23)``, no clean shutdown: connections drop mid-request), once per process;
 * ``kill_rank_at_step:R@N`` -- rank R of a sync-DP job dies abruptly (``os._exit(23)``) when it is about to
   run training step N (examples/ResNet50/resnet50_train.py; the survivors' watchdog or collective reports it);
+* ``kill_worker_at_run:T@N`` -- worker task T of a PS job dies abruptly at its N-th session run
+  (train/session.py; its PS connection drops mid-job: backup workers / timeouts must cope);
 * ``drop_grad:P``        -- a worker silently drops each gradient push with probability P (a lost
   update; the async algorithms must tolerate it, sync ones need backup workers);
 * ``seed:S``             -- seed of the drop decisions (default 0).
@@ -49,6 +51,18 @@ def maybe_kill_rank(rank, step):
     if int(r) == int(rank) and int(n) == int(step):
         import sys
         print("dtg.fault: killing rank %d at step %d" % (rank, step), file=sys.stderr, flush=True)
+        os._exit(KILL_EXIT_CODE)
+
+
+def maybe_kill_worker(task, run):
+    """``kill_worker_at_run:T@N``: die like a crashed process if this is worker task T at its N-th run."""
+    v = _parse().get("kill_worker_at_run")
+    if not v:
+        return
+    t, _, n = v.partition("@")
+    if int(t) == int(task) and int(n) == int(run):
+        import sys
+        print("dtg.fault: killing worker %d at run %d" % (task, run), file=sys.stderr, flush=True)
         os._exit(KILL_EXIT_CODE)
 
 

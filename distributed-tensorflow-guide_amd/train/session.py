@@ -182,6 +182,11 @@ class _Session:
         # bootstrap runs crash when a finished job is resumed from its checkpoint (the first run's
         # StopAtStepHook already requests the stop).  dtg keeps running the fetches; the training
         # loop's should_stop() check then ends the job cleanly.
+        self._runs = getattr(self, "_runs", 0) + 1
+        if fault.config().get("kill_worker_at_run"):
+            srv = _this_server()
+            if srv is not None and srv.job_name == "worker":
+                fault.maybe_kill_worker(srv.task_index, self._runs)
         rc = SessionRunContext(SessionRunArgs(fetches, feed_dict), self)
         hargs = [h.before_run(rc) for h in self.hooks]
         feed = dict(feed_dict or {})

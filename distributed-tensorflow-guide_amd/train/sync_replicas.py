@@ -16,6 +16,7 @@ Two execution modes behind one API:
   all-reduce overlapped with backward -- the fast path for the north-star models.  See
   ``SyncReplicasOptimizer.allreduce()``.
 """
+import os
 import threading
 import time
 
@@ -49,6 +50,8 @@ class SyncReplicasOptimizer(Optimizer):
         # strict lock-step (dtg extension, enabled by num_tokens == 0 in the hook): one token queue
         # per worker, so every replica contributes exactly one fresh gradient per global step
         self.strict = False
+        # seconds a worker waits for the chief's next token before failing (a lost worker without backups)
+        self.sync_timeout = float(os.environ.get("DTG_SYNC_TIMEOUT", "600"))
 
     def _token_queue(self, task=None):
         if not self.strict:
@@ -115,15 +118,30 @@ class SyncReplicasOptimizer(Optimizer):
 
     # ---- chief aggregation loop (TF: get_chief_queue_runner) ---------------------------------
     def _chief_loop(self):
+        from ..variables import new_client
         opt = self._opt
         gv = self._gv
         gs = self._global_step
+        conns = {}
+
+        def cl(v):  # this thread's own connections: its blocking acc_take must not starve the training thread
+            c = conns.get(v.ps_task)
+            if c is None:
+                c = conns[v.ps_task] = new_client(*v.ps_task)
+            return c
+        try:
+            self._chief_steps(opt, gv, gs, cl)
+        finally:
+            for c in conns.values():
+                c.close()
+
+    def _chief_steps(self, opt, gv, gs, cl):
         while not self._chief_stop.is_set():
             grads = []
             for _, v in gv:
                 g = None
                 while g is None and not self._chief_stop.is_set():
-                    g = v._client().acc_take(self._acc_name(v), self._replicas_to_aggregate, 0.25)
+                    g = cl(v).acc_take(self._acc_name(v), self._replicas_to_aggregate, 0.25)
                 if g is None:
                     return
                 grads.append(g)
@@ -135,19 +153,19 @@ class SyncReplicasOptimizer(Optimizer):
             new_step = None
             for task, items in by_task.items():
                 gs_name = gs._name if (gs.remote and gs.ps_task == task and new_step is None) else ""
-                client = [v for _, v in gv if v.ps_task == task][0]._client()
+                client = cl([v for _, v in gv if v.ps_task == task][0])
                 step, _ = client.apply(opt.PS_KIND, opt._hyper(lr), bool(opt._use_locking), gs_name, items, False)
                 if gs_name:
                     new_step = step
             if new_step is None:
-                new_step = int(gs._client().assign_add(gs._name, np.ones((), _np(gs.dtype))))
+                new_step = int(cl(gs).assign_add(gs._name, np.ones((), _np(gs.dtype))))
             for _, v in gv:
-                v._client().acc_set_step(self._acc_name(v), int(new_step))
+                cl(v).acc_set_step(self._acc_name(v), int(new_step))
             if self.strict:
                 for t in range(self._total_num_replicas):
-                    self._gs_client().q_enqueue(self._token_queue(t), [int(new_step)])
+                    cl(gs).q_enqueue(self._token_queue(t), [int(new_step)])
             else:
-                self._gs_client().q_enqueue(TOKEN_QUEUE, [int(new_step)] * self._tokens_per_step)
+                cl(gs).q_enqueue(TOKEN_QUEUE, [int(new_step)] * self._tokens_per_step)
 
     def start_chief(self):
         if self._chief_thread is None:
@@ -164,6 +182,10 @@ class SyncReplicasOptimizer(Optimizer):
 
 def _np(dt):
     return {torch.int32: np.int32, torch.int64: np.int64}.get(dt, np.float32)
+
+
+class SyncTimeoutError(RuntimeError):
+    """A synchronous step could not be aggregated in time (TF: DeadlineExceededError)."""
 
 
 class _ReadyForLocalInit(Tensor):
@@ -193,6 +215,8 @@ class _SyncTrainOp(Op):
             if not ok:
                 sro.dropped += 1
         client = sro._gs_client()
+        import time
+        t0 = time.monotonic()
         while True:
             tok = client.q_dequeue(sro._token_queue(), 0.5)
             if tok is not None:
@@ -201,6 +225,12 @@ class _SyncTrainOp(Op):
             sess = ctx.session
             if sess is not None and sess._stop_requested_externally():
                 return None
+            if time.monotonic() - t0 > sro.sync_timeout:
+                raise SyncTimeoutError(
+                    "SyncReplicasOptimizer: no aggregated step for %.0f s -- fewer than replicas_to_aggregate=%d "
+                    "workers are pushing gradients (a worker may be lost).  With total_num_replicas > "
+                    "replicas_to_aggregate the surplus workers are backups and the job survives such a loss."
+                    % (sro.sync_timeout, sro._replicas_to_aggregate))
 
 
 class _SyncReplicasHook(SessionRunHook):

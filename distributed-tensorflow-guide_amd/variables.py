@@ -44,13 +44,30 @@ def client_for(job, task, timeout=120.0):
             from . import _runtime
             host, port = addr.rsplit(":", 1)
             c = _runtime.PSClient("127.0.0.1" if host == "localhost" else host, int(port), timeout)
+            s = _this_server()
+            if s is not None and s.job_name == "worker" and job == "ps":
+                # if this worker process dies, the PS counts it as finished instead of joining forever
+                c.watch("__worker__", s.task_index)
             _conns[addr] = c
         return c
+
+
+def new_client(job, task, timeout=120.0):
+    """A private connection (not shared through client_for): for a thread that makes long blocking calls
+    (the SyncReplicas chief's accumulator waits), so it never holds the shared connection's lock against
+    the training thread."""
+    from . import _runtime
+    host, port = task_address(job, task).rsplit(":", 1)
+    return _runtime.PSClient("127.0.0.1" if host == "localhost" else host, int(port), timeout)
 
 
 def close_connections():
     with _conn_lock:
         for c in _conns.values():
+            try:
+                c.unwatch()
+            except Exception:
+                pass
             try:
                 c.close()
             except Exception:

@@ -234,3 +234,16 @@ def test_notebook_shared_ps_protocol():
     assert val("a_global seen by worker 2:")[0] == pytest.approx(x0 + 0.1, abs=1e-6)
     after2 = val("a_global after worker 2 update:")
     assert len(after2) == 2 and all(v == pytest.approx(x0 + 0.2, abs=1e-6) for v in after2)
+
+
+@pytest.mark.gpu
+def test_multi_gpu_example_workers_on_gpu(tmp_path):
+    """The Multiple-GPUs-Single-Machine example with its workers' compute on the GPU (both on cuda:0 of a
+    one-GPU box; one GPU per worker through HIP_VISIBLE_DEVICES on a node, dist_mult_gpu_sing_mach.sh;
+    reference dist_mult_gpu_sing_mach.py:31-39): ConfigProto.hip_device / placement resolve to cuda."""
+    out = run_cluster("Multiple-GPUs-Single-Machine/dist_mult_gpu_sing_mach.py", 1, 2,
+                      ["--steps", "30", "--logdir", str(tmp_path / "l")], timeout=240)
+    _ok(out)
+    for t in range(2):
+        w = out[("worker", t)][1]
+        assert "worker %d computes on cuda:0" % t in w, w[-2000:]

@@ -78,3 +78,29 @@ def test_dropped_gradient_pushes_are_lost_updates(tmp_path):
     res = json.loads([l for l in w_out.splitlines() if l.startswith("RESULT ")][-1][len("RESULT "):])
     assert res["final_step"] >= 30
     assert res["local_runs"] > 1.4 * res["final_step"], res
+
+
+def test_ssgd_backup_workers_survive_a_dead_worker():
+    """SURVEY §4.2 fault injection, sync mode: 3 workers aggregating 2 per step (one backup); worker 2 dies at
+    its 3rd run.  The chief keeps aggregating the two live workers' gradients to the last step, and the PS
+    counts the dead worker as finished (its watched connection dropped) so it exits too."""
+    from _cluster import last_int_after, run_cluster
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 3, ["--init_tokens", "0"],
+                      env={"DTG_FAULT": "kill_worker_at_run:2@3"}, timeout=120)
+    assert out[("worker", 2)][0] == 23
+    for t in (0, 1):
+        rc, o = out[("worker", t)]
+        assert rc == 0, o[-2000:]
+    assert last_int_after(out[("worker", 0)][1], "step: ") >= 10
+    assert out[("ps", 0)][0] == 0
+
+
+def test_ssgd_without_backups_fails_cleanly_on_a_dead_worker():
+    """Same loss without a backup (2 of 2): the survivor cannot complete a step; it fails with a clear
+    SyncTimeoutError (TF: DeadlineExceededError) instead of waiting forever."""
+    from _cluster import run_cluster
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 2, ["--init_tokens", "0"],
+                      env={"DTG_FAULT": "kill_worker_at_run:1@3", "DTG_SYNC_TIMEOUT": "20"}, timeout=120)
+    assert out[("worker", 1)][0] == 23
+    rc, o = out[("worker", 0)]
+    assert rc != 0 and "SyncTimeoutError" in o and "a worker may be lost" in o, o[-2000:]
