@@ -282,6 +282,104 @@ Tensor attn_fused_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, c10::opti
 
 namespace py = pybind11;
 
+
+// ---- BERT heads (heads.hip) -------------------------------------------------------------------------
+static const long long* i64p(const Tensor& t) { return reinterpret_cast<const long long*>(t.data_ptr<int64_t>()); }
+
+// rows of src [B*S, H] at (i / P) * S + pos[i] -> [B*P, H]
+Tensor gather_rows(Tensor src, Tensor pos, int64_t S) {
+  CHECK_GPU_BF16_CONTIG(src);
+  TORCH_CHECK(pos.scalar_type() == at::kLong && pos.is_contiguous() && pos.dim() == 2, "pos: [B, P] int64");
+  const int H = (int)src.size(1), P = (int)pos.size(1), R = (int)pos.numel();
+  TORCH_CHECK(H % 8 == 0 && src.size(0) == pos.size(0) * S, "gather_rows shape mismatch");
+  c10::DeviceGuard dg(src.device());
+  Tensor out = at::empty({R, H}, src.options());
+  dtg::gather_rows(cbfp(src), i64p(pos), bfp(out), R, P, (int)S, H, cur_stream());
+  return out;
+}
+
+// dst rows (i / P) * S + pos[i] += src[i]; without pos: dst rows i * S (the [CLS] rows) += src[i]
+void scatter_rows_add(Tensor dst, c10::optional<Tensor> pos, Tensor src, int64_t S) {
+  CHECK_GPU_BF16_CONTIG(dst);
+  CHECK_GPU_BF16_CONTIG(src);
+  const int H = (int)dst.size(1), R = (int)src.size(0);
+  TORCH_CHECK(src.size(1) == H && H % 8 == 0, "scatter_rows_add width mismatch");
+  int P = 1;
+  if (has(pos)) {
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->is_contiguous() && pos->dim() == 2 && pos->numel() == R,
+                "pos: [B, P] int64");
+    P = (int)pos->size(1);
+    TORCH_CHECK(dst.size(0) == pos->size(0) * S, "scatter_rows_add rows");
+  } else {
+    TORCH_CHECK(dst.size(0) == (int64_t)R * S, "scatter_rows_add rows");
+  }
+  c10::DeviceGuard dg(dst.device());
+  dtg::scatter_rows_add(bfp(dst), has(pos) ? i64p(*pos) : nullptr, cbfp(src), R, P, (int)S, H, cur_stream());
+}
+
+// -> (total loss [] fp32 = mean NSP cross-entropy + extra, softmax probabilities [B, 2] fp32)
+std::vector<Tensor> nsp_loss_fwd(Tensor pooled, Tensor wn, Tensor bn, Tensor labels, c10::optional<Tensor> extra) {
+  CHECK_GPU_BF16_CONTIG(pooled);
+  CHECK_GPU_BF16_CONTIG(wn);
+  CHECK_F32_CONTIG(bn);
+  const int B = (int)pooled.size(0), H = (int)pooled.size(1);
+  TORCH_CHECK(wn.size(0) == 2 && wn.size(1) == H && bn.numel() == 2 && H % 8 == 0, "NSP head is [2, H]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == B, "labels [B] int64");
+  if (has(extra)) CHECK_F32_CONTIG(*extra);
+  c10::DeviceGuard dg(pooled.device());
+  Tensor probs = at::empty({B, 2}, pooled.options().dtype(at::kFloat));
+  Tensor out = at::empty({}, pooled.options().dtype(at::kFloat));
+  dtg::nsp_loss_fwd(cbfp(pooled), cbfp(wn), bn.data_ptr<float>(), i64p(labels),
+                    has(extra) ? extra->data_ptr<float>() : nullptr, probs.data_ptr<float>(), out.data_ptr<float>(), B,
+                    H, cur_stream());
+  return {out, probs};
+}
+
+// -> dpre [B, H] bf16 (gradient before the pooler's tanh); accumulates gwn (bf16 [2, H]) and gbn (fp32 [2])
+Tensor nsp_loss_bwd(Tensor pooled, Tensor wn, Tensor probs, Tensor labels, Tensor gout, Tensor gwn, Tensor gbn) {
+  CHECK_GPU_BF16_CONTIG(pooled);
+  CHECK_GPU_BF16_CONTIG(wn);
+  CHECK_GPU_BF16_CONTIG(gwn);
+  CHECK_F32_CONTIG(probs);
+  CHECK_F32_CONTIG(gout);
+  CHECK_F32_CONTIG(gbn);
+  const int B = (int)pooled.size(0), H = (int)pooled.size(1);
+  TORCH_CHECK(gwn.numel() == 2 * H && gbn.numel() == 2 && probs.numel() == 2 * B && labels.numel() == B, "shapes");
+  c10::DeviceGuard dg(pooled.device());
+  Tensor dpre = at::empty_like(pooled);
+  dtg::nsp_loss_bwd(cbfp(pooled), cbfp(wn), probs.data_ptr<float>(), i64p(labels), gout.data_ptr<float>(), bfp(dpre),
+                    bfp(gwn), gbn.data_ptr<float>(), B, H, cur_stream());
+  return dpre;
+}
+
+Tensor row_sum(Tensor x, double scale) {
+  CHECK_F32_CONTIG(x);
+  c10::DeviceGuard dg(x.device());
+  Tensor out = at::empty({}, x.options());
+  dtg::row_sum(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), (float)scale, cur_stream());
+  return out;
+}
+
+// sort-free word-embedding gradient: gW[ids[t]] += ds[t] (vocab rows owned per workgroup, token order)
+bool emb_word_bwd_owned(Tensor ds, Tensor ids, Tensor gW) {
+  CHECK_GPU_BF16_CONTIG(ds);
+  CHECK_GPU_BF16_CONTIG(gW);
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous(), "ids int64");
+  const int T = (int)ds.size(0), H = (int)ds.size(1), V = (int)gW.size(0);
+  TORCH_CHECK(ids.numel() == T && gW.size(1) == H && H % 8 == 0, "shape mismatch");
+  if ((long long)32 * H * 4 > 131072) return false;  // accumulator tile does not fit LDS: caller sorts instead
+  c10::DeviceGuard dg(ds.device());
+  dtg::emb_word_bwd_owned(cbfp(ds), i64p(ids), bfp(gW), T, H, V, cur_stream());
+  return true;
+}
+
+// stream-ordered zero fill (hipMemsetAsync: a DMA fill, no framework kernel)
+void zero_(Tensor t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
+  c10::DeviceGuard dg(t.device());
+  C10_HIP_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()));
+}
+
 void register_transformer_ops(py::module_& m) {
   m.def("gemm_strided_batched", &gemm_strided_batched);
   m.def("ln_fwd", &ln_fwd, py::arg("h"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("eps") = 1e-12,
@@ -299,5 +397,12 @@ void register_transformer_ops(py::module_& m) {
   m.def("attn_fused_bwd", &attn_fused_bwd);
   m.def("attn_fused_supported", [](int64_t S, int64_t dh, bool bwd) { return dtg::attn_fused_supported(S, dh, bwd) != 0; });
   m.def("emb_word_bwd", &emb_word_bwd);
+  m.def("gather_rows", &gather_rows);
+  m.def("scatter_rows_add", &scatter_rows_add);
+  m.def("nsp_loss_fwd", &nsp_loss_fwd);
+  m.def("nsp_loss_bwd", &nsp_loss_bwd);
+  m.def("row_sum", &row_sum);
+  m.def("emb_word_bwd_owned", &emb_word_bwd_owned);
+  m.def("zero_", &zero_);
   m.def("emb_pos_bwd", &emb_pos_bwd);
 }

@@ -11,7 +11,7 @@ struct Epi {
   int c_bf16;
   float alpha, beta;
   const float* bias;  // per column (N), may be null
-  int act;            // 0 none, 1 relu, 2 gelu(tanh)
+  int act;            // 0 none, 1 relu, 2 gelu(tanh), 3 tanh (BERT pooler)
   void* aux = nullptr;  // bf16 [M, ldc] side buffer (see aux_mode)
   // 0 none; 1 store the pre-activation to aux; 2 multiply by act'(aux) (act backward from the saved
   // pre-activation); 3 store act'(pre-activation) to aux (forward: the derivative while the
@@ -27,9 +27,15 @@ __device__ __forceinline__ float gelu_sig(float x) {  // sigmoid(2u), u = sqrt(2
   return __builtin_amdgcn_rcpf(1.f + __expf(-u2));
 }
 
+// tanh(x) = 2 sigmoid(2x) - 1: one v_exp_f32 + one v_rcp_f32 (saturates cleanly to +-1)
+__device__ __forceinline__ float tanh_fast(float x) {
+  return fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)), -1.f);
+}
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == 1) return fmaxf(v, 0.f);
   if (act == 2) return v * gelu_sig(v);
+  if (act == 3) return tanh_fast(v);
   return v;
 }
 
@@ -40,6 +46,10 @@ __device__ __forceinline__ float act_grad(float x, int act) {
     const float s = gelu_sig(x);
     const float du = 0.7978845608028654f * fmaf(3.f * 0.044715f * x, x, 1.f);
     return fmaf(2.f * x * s * (1.f - s), du, s);
+  }
+  if (act == 3) {
+    const float t = tanh_fast(x);
+    return fmaf(-t, t, 1.f);
   }
   return 1.f;
 }
@@ -168,6 +178,9 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
   } else if (e.act == 2) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] *= gelu_sig(v[k]);
+  } else if (e.act == 3) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tanh_fast(v[k]);
   }
   store8_bf16(p, v);
 }

@@ -160,6 +160,17 @@ void emb_word_bwd(const bf16_t* ds, const long long* sorted, const long long* pe
                   hipStream_t st);
 void emb_pos_bwd(const bf16_t* ds, bf16_t* gP, int T, int S, int H, hipStream_t st);
 
+// ---- BERT pre-training heads and row plumbing (heads.hip) -----------------------------------------
+void gather_rows(const bf16_t* src, const long long* pos, bf16_t* out, int R, int P, int S, int H, hipStream_t st);
+void scatter_rows_add(bf16_t* dst, const long long* pos, const bf16_t* src, int R, int P, int S, int H,
+                      hipStream_t st);
+void nsp_loss_fwd(const bf16_t* pooled, const bf16_t* wn, const float* bn, const long long* labels, const float* extra,
+                  float* probs, float* out, int B, int H, hipStream_t st);
+void nsp_loss_bwd(const bf16_t* pooled, const bf16_t* wn, const float* probs, const long long* labels, const float* gout,
+                  bf16_t* dpre, bf16_t* gwn, float* gbn, int B, int H, hipStream_t st);
+void row_sum(const float* x, float* out, long long n, float scale, hipStream_t st);
+void emb_word_bwd_owned(const bf16_t* ds, const long long* ids, bf16_t* gW, int T, int H, int V, hipStream_t st);
+
 // ---- fused attention, head dim 64 (attention.hip) ---------------------------------------------
 int attn_fused_supported(int S, int dh, int backward);
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,

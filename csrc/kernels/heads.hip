@@ -1,0 +1,282 @@
+// BERT pre-training heads and their row plumbing, so the whole loss runs on dtg kernels (no vendor GEMM,
+// no sort, no framework loss or index kernels on the step):
+//
+//   gather_rows        hm[i] = seq[(i / P) * S + pos[i]]          masked-LM rows (pos: [B, P] positions)
+//   scatter_rows_add   dseq[(i / P) * S + pos[i]] += dhm[i]         (pos == null: rows i * S, the [CLS] rows)
+//   nsp_loss_fwd       logits = pooled Wn^T + bn ([B, 2]), softmax cross-entropy, mean over B, + the MLM
+//                      loss -> the total pre-training loss (one workgroup: a deterministic reduction order)
+//   nsp_loss_bwd       dlogits = (p - onehot) * g / B;  dpre = (dlogits Wn) * (1 - pooled^2)  (tanh');
+//                      dWn += dlogits^T pooled;  dbn += colsum(dlogits)
+//   row_sum            out = scale * sum(x)  (the MLM loss from the per-row cross-entropies)
+//   emb_word_bwd_owned dWemb[v] += sum_{t: ids[t] = v} ds[t]: each workgroup OWNS a tile of vocabulary rows,
+//                      scans the ids for its tile and adds the matching rows in token order -- sort-free,
+//                      no atomics, deterministic (replaces a radix sort + per-run reduction)
+//
+// Reference: the reference trains a 2-parameter toy; this is BASELINE.json config 5 (BERT-base).
+#include "dtg/common.h"
+#include "dtg/kernels.h"
+
+namespace dtg {
+
+namespace {
+
+// one wave per row, 8 columns per lane per step
+__global__ void __launch_bounds__(256) gather_rows_kernel(const bf16_t* __restrict__ src, const long long* __restrict__ pos,
+                                                          bf16_t* __restrict__ out, int R, int P, int S, int H) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= R) return;
+  const long long row = (long long)(i / P) * S + pos[i];
+  const uint4* s = reinterpret_cast<const uint4*>(src + row * H);
+  uint4* d = reinterpret_cast<uint4*>(out + (long long)i * H);
+  for (int c = lane; c < (H >> 3); c += 64) d[c] = s[c];
+}
+
+__global__ void __launch_bounds__(256) scatter_rows_add_kernel(bf16_t* __restrict__ dst, const long long* __restrict__ pos,
+                                                               const bf16_t* __restrict__ src, int R, int P, int S, int H) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= R) return;
+  const long long row = pos ? (long long)(i / P) * S + pos[i] : (long long)i * S;
+  for (int c = lane; c < (H >> 3); c += 64) {
+    float a[8], b[8];
+    load8_bf16(dst + row * H + c * 8, a);
+    load8_bf16(src + (long long)i * H + c * 8, b);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += b[k];
+    store8_bf16(dst + row * H + c * 8, a);
+  }
+}
+
+constexpr int kNspThreads = 1024;
+
+// single workgroup: wave w takes rows w, w + 16, ...; lane 0 keeps the wave's loss sum; the 16 wave sums
+// are added in wave order
+__global__ void __launch_bounds__(kNspThreads) nsp_loss_fwd_kernel(const bf16_t* __restrict__ pooled,
+                                                                  const bf16_t* __restrict__ wn,
+                                                                  const float* __restrict__ bn,
+                                                                  const long long* __restrict__ labels,
+                                                                  const float* __restrict__ extra,
+                                                                  float* __restrict__ probs, float* __restrict__ out,
+                                                                  int B, int H) {
+  __shared__ float wsum[kNspThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int b = wave; b < B; b += kNspThreads / 64) {
+    float d0 = 0.f, d1 = 0.f;
+    for (int c = lane; c < (H >> 3); c += 64) {
+      float x[8], w0[8], w1[8];
+      load8_bf16(pooled + (long long)b * H + c * 8, x);
+      load8_bf16(wn + c * 8, w0);
+      load8_bf16(wn + H + c * 8, w1);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        d0 = fmaf(x[k], w0[k], d0);
+        d1 = fmaf(x[k], w1[k], d1);
+      }
+    }
+    d0 = wave_sum(d0) + bn[0];
+    d1 = wave_sum(d1) + bn[1];
+    const float m = fmaxf(d0, d1);
+    const float e0 = __expf(d0 - m), e1 = __expf(d1 - m);
+    const float lse = m + __logf(e0 + e1);
+    const long long y = labels[b];
+    if (lane == 0) {
+      probs[2 * b] = e0 / (e0 + e1);
+      probs[2 * b + 1] = e1 / (e0 + e1);
+      if (y >= 0) acc += lse - (y == 0 ? d0 : d1);
+    }
+  }
+  if (lane == 0) wsum[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < kNspThreads / 64; ++w) t += wsum[w];
+    out[0] = t / (float)B + (extra ? extra[0] : 0.f);
+  }
+}
+
+// grid: H / 64 workgroups of 64 columns x 16 batch groups; column reductions over the batch through LDS in a
+// fixed order (deterministic)
+__global__ void __launch_bounds__(1024) nsp_loss_bwd_kernel(const bf16_t* __restrict__ pooled,
+                                                           const bf16_t* __restrict__ wn,
+                                                           const float* __restrict__ probs,
+                                                           const long long* __restrict__ labels,
+                                                           const float* __restrict__ gout, bf16_t* __restrict__ dpre,
+                                                           bf16_t* __restrict__ gwn, float* __restrict__ gbn, int B, int H) {
+  __shared__ float red[2][16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int h = blockIdx.x * 64 + tx;
+  const float g = gout[0] / (float)B;
+  const float w0 = h < H ? bf2f(wn[h]) : 0.f, w1 = h < H ? bf2f(wn[H + h]) : 0.f;
+  float a0 = 0.f, a1 = 0.f;
+  for (int b = ty; b < B; b += 16) {
+    const long long y = labels[b];
+    const float s = y >= 0 ? g : 0.f;
+    const float l0 = (probs[2 * b] - (y == 0 ? 1.f : 0.f)) * s;
+    const float l1 = (probs[2 * b + 1] - (y == 1 ? 1.f : 0.f)) * s;
+    if (h < H) {
+      const float p = bf2f(pooled[(long long)b * H + h]);
+      dpre[(long long)b * H + h] = f2bf((l0 * w0 + l1 * w1) * fmaf(-p, p, 1.f));
+      a0 = fmaf(l0, p, a0);
+      a1 = fmaf(l1, p, a1);
+    }
+  }
+  red[0][ty][tx] = a0;
+  red[1][ty][tx] = a1;
+  __syncthreads();
+  if (ty == 0 && h < H) {
+    float t0 = 0.f, t1 = 0.f;
+    for (int k = 0; k < 16; ++k) {
+      t0 += red[0][k][tx];
+      t1 += red[1][k][tx];
+    }
+    gwn[h] = f2bf(bf2f(gwn[h]) + t0);
+    gwn[H + h] = f2bf(bf2f(gwn[H + h]) + t1);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) {
+    const int c = threadIdx.x;
+    float t = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const long long y = labels[b];
+      if (y >= 0) t += (probs[2 * b + c] - (y == c ? 1.f : 0.f)) * g;
+    }
+    gbn[c] += t;
+  }
+}
+
+__global__ void __launch_bounds__(1024) row_sum_kernel(const float* __restrict__ x, float* __restrict__ out, long long n,
+                                                      float scale) {
+  __shared__ float wsum[16];
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 1024) acc += x[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += wsum[w];
+    out[0] = t * scale;
+  }
+}
+
+// Word-embedding gradient, sort-free.  Workgroup w owns vocabulary rows [w*VT, (w+1)*VT).  It walks the ids in
+// chunks of 256 (one per thread), compacts the matching token indices IN TOKEN ORDER into an LDS list (wave
+// ballots + a prefix over the 4 waves), and whenever the list fills (or at the end) adds the listed rows of ds
+// into an fp32 LDS accumulator [VT][H]: thread t owns 8-column chunks t, t + 256, ... and walks the list in
+// order, so every vocabulary row is summed in token order by exactly one thread per chunk -- deterministic
+// without atomics.  Rows that received anything are added once into the bf16 gradient.
+constexpr int kEmbVT = 32, kEmbList = 512;
+
+__global__ void __launch_bounds__(256) emb_word_bwd_owned_kernel(const bf16_t* __restrict__ ds,
+                                                                const long long* __restrict__ ids,
+                                                                bf16_t* __restrict__ gW, int T, int H, int V) {
+  extern __shared__ float acc[];                       // [kEmbVT][H]
+  __shared__ int list[kEmbList];
+  __shared__ int wcount[4];
+  __shared__ int nlist_s;
+  __shared__ int touched[kEmbVT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int v0 = blockIdx.x * kEmbVT;
+  const int nch = H >> 3;
+  for (int i = tid; i < kEmbVT * H; i += 256) acc[i] = 0.f;
+  if (tid < kEmbVT) touched[tid] = 0;
+  if (tid == 0) nlist_s = 0;
+  __syncthreads();
+  auto flush = [&](int n) {
+    for (int c = tid; c < nch; c += 256) {
+      for (int j = 0; j < n; ++j) {
+        const int t = list[j];
+        const int r = (int)(ids[t] - v0);
+        float x[8];
+        load8_bf16(ds + (long long)t * H + c * 8, x);
+        float* a = acc + r * H + c * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += x[k];
+      }
+    }
+  };
+  for (int base = 0; base < T; base += 256) {
+    const int t = base + tid;
+    const long long id = t < T ? ids[t] : -1;
+    const bool hit = id >= v0 && id < v0 + kEmbVT && id < V;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wcount[wave] = __popcll(m);
+    __syncthreads();
+    int off = nlist_s;
+    for (int w = 0; w < wave; ++w) off += wcount[w];
+    const int total = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    if (nlist_s + total > kEmbList) {  // flush the list first (every thread sees the same condition)
+      const int n = nlist_s;
+      flush(n);
+      __syncthreads();
+      off -= n;
+      if (tid == 0) nlist_s = 0;
+    }
+    if (hit) {
+      const int rank = __popcll(m & ((1ull << lane) - 1ull));
+      list[off + rank] = t;
+      touched[(int)(id - v0)] = 1;
+    }
+    __syncthreads();
+    if (tid == 0) nlist_s += total;
+    __syncthreads();
+  }
+  flush(nlist_s);
+  __syncthreads();
+  for (int r = 0; r < kEmbVT && v0 + r < V; ++r) {
+    if (!touched[r]) continue;
+    for (int c = tid; c < nch; c += 256) {
+      float o[8];
+      bf16_t* g = gW + (long long)(v0 + r) * H + c * 8;
+      load8_bf16(g, o);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += acc[r * H + c * 8 + k];
+      store8_bf16(g, o);
+    }
+  }
+}
+
+}  // namespace
+
+void gather_rows(const bf16_t* src, const long long* pos, bf16_t* out, int R, int P, int S, int H, hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((R + 3) / 4), dim3(256), 0, st, src, pos, out, R, P, S, H);
+}
+
+void scatter_rows_add(bf16_t* dst, const long long* pos, const bf16_t* src, int R, int P, int S, int H,
+                      hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(scatter_rows_add_kernel, dim3((R + 3) / 4), dim3(256), 0, st, dst, pos, src, R, P, S, H);
+}
+
+void nsp_loss_fwd(const bf16_t* pooled, const bf16_t* wn, const float* bn, const long long* labels, const float* extra,
+                  float* probs, float* out, int B, int H, hipStream_t st) {
+  hipLaunchKernelGGL(nsp_loss_fwd_kernel, dim3(1), dim3(kNspThreads), 0, st, pooled, wn, bn, labels, extra, probs, out,
+                     B, H);
+}
+
+void nsp_loss_bwd(const bf16_t* pooled, const bf16_t* wn, const float* probs, const long long* labels, const float* gout,
+                  bf16_t* dpre, bf16_t* gwn, float* gbn, int B, int H, hipStream_t st) {
+  hipLaunchKernelGGL(nsp_loss_bwd_kernel, dim3((H + 63) / 64), dim3(1024), 0, st, pooled, wn, probs, labels, gout, dpre,
+                     gwn, gbn, B, H);
+}
+
+void row_sum(const float* x, float* out, long long n, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(row_sum_kernel, dim3(1), dim3(1024), 0, st, x, out, n, scale);
+}
+
+void emb_word_bwd_owned(const bf16_t* ds, const long long* ids, bf16_t* gW, int T, int H, int V, hipStream_t st) {
+  const size_t lds = (size_t)kEmbVT * H * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)emb_word_bwd_owned_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+    attr = true;
+  }
+  hipLaunchKernelGGL(emb_word_bwd_owned_kernel, dim3((V + kEmbVT - 1) / kEmbVT), dim3(256), lds, st, ds, ids, gW, T, H,
+                     V);
+  DTG_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtg

@@ -119,6 +119,7 @@ class BertForPreTraining(nn.Module):
         self.nsp_w = _normal((2, H), s)
         self.nsp_b = _zeros(2)
         self.fused = True
+        self.fused_heads = True  # MLM + NSP heads + losses as one node on dtg kernels (bert_fused.heads_loss)
         self.seed = seed
         self._step = 0
 
@@ -147,7 +148,6 @@ class BertForPreTraining(nn.Module):
         p_h = cfg.dropout if self.training else 0.0
         p_a = cfg.attn_dropout if self.training else 0.0
         mask_add = T.mask_additive(attention_mask) if attention_mask is not None else None
-        flat_pos = (mlm_positions + torch.arange(B, device=ids.device).unsqueeze(1) * S).reshape(-1)
         labels = mlm_labels.reshape(-1)
         nv = labels.numel() if num_valid is None else num_valid
         if self.fused_ok(ids):
@@ -155,15 +155,22 @@ class BertForPreTraining(nn.Module):
             for i, layer in enumerate(self.layers):
                 seq = bert_fused.encoder_layer(layer, seq, mask_add, B, S, cfg, p_h, p_a, self._seed(i + 1, 1),
                                                self._seed(i + 1, 2), self._seed(i + 1, 3))
-            mlm = bert_fused.mlm_head(self, seq.index_select(0, flat_pos), labels, nv)
+            if self.fused_heads and mlm_positions.dtype == torch.long and nsp_labels.dtype == torch.long:
+                return bert_fused.heads_loss(self, seq, mlm_positions, mlm_labels, nsp_labels, nv, B, S)
+            mlm = bert_fused.mlm_head(self, seq.index_select(0, self._flat_pos(mlm_positions, S)), labels, nv)
         else:
             seq = self._reference_encoder(ids, token_types, mask_add, p_h, p_a)
-            mlm = self._reference_mlm(seq.index_select(0, flat_pos), labels, nv)
+            mlm = self._reference_mlm(seq.index_select(0, self._flat_pos(mlm_positions, S)), labels, nv)
         cls = seq.view(B, S, -1)[:, 0]
         pooled = torch.tanh(F.linear(cls, self.pool_w, self.pool_b.to(cls.dtype)))
         nsp_logits = F.linear(pooled, self.nsp_w, self.nsp_b.to(pooled.dtype))
         nsp = F.cross_entropy(nsp_logits.float(), nsp_labels)
         return mlm + nsp
+
+    @staticmethod
+    def _flat_pos(mlm_positions, S):
+        B = mlm_positions.shape[0]
+        return (mlm_positions + torch.arange(B, device=mlm_positions.device).unsqueeze(1) * S).reshape(-1)
 
     # -- plain PyTorch path (CPU, and the oracle of the fused path) -------------------------------------------
     def _reference_encoder(self, ids, token_types, mask_add, p_h, p_a):

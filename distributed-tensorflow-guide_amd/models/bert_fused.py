@@ -167,8 +167,9 @@ class _EmbFn(torch.autograd.Function):
         accs = [_gacc(q) for q in ctx.mod_params]
         (gw, _), (gp, _), (gt, _), (gg, _), (gb, _) = accs
         ds, _ = L.ln_bwd(dy.contiguous(), s, g, mean, rstd, gg, gb, 0.0, 0, p, seed, False)
-        srt, perm = torch.sort(ids)
-        L.emb_word_bwd(ds, srt, perm, gw)
+        if not L.emb_word_bwd_owned(ds, ids, gw):  # sort-free, deterministic (heads.hip); wide H: sort
+            srt, perm = torch.sort(ids)
+            L.emb_word_bwd(ds, srt, perm, gw)
         L.emb_pos_bwd(ds, gp, S)
         if tt is not None:
             L.colsum(ds, gt.view(-1), True, tt, typ.shape[0])
@@ -230,3 +231,80 @@ def mlm_head(model, hm, labels, num_valid):
     params = [model.mlm_w, model.mlm_b, model.mlm_ln_g, model.mlm_ln_b, model.emb.word, model.mlm_bias]
     return _MLMFn.apply(hm.contiguous(), labels.contiguous(), (model.cfg.eps, float(num_valid)), _Holder(params),
                         *params)
+
+
+# ---- both pre-training heads and the total loss as ONE node ----------------------------------------------
+class _HeadsFn(torch.autograd.Function):
+    """Masked-LM head (gather -> transform GEMM + GELU -> LN -> tied decoder GEMM -> softmax-xent) and the
+    next-sentence head ([CLS] rows -> pooler GEMM with tanh epilogue -> 2-way softmax-xent) plus the sum of
+    the two losses, all on dtg kernels (heads.hip, gemm.hip, softmax_xent.hip, transformer.hip): no
+    index_select / slice / F.linear / F.cross_entropy on the step, and ``seq``'s gradient is assembled by
+    a stream-ordered zero fill + two row scatters."""
+
+    @staticmethod
+    def forward(ctx, seq, pos, labels, nsp_labels, geom, holder, w_t, b_t, g, b, word, dec_bias, pool_w, pool_b,
+                nsp_w, nsp_b):
+        L = lib()
+        eps, denom, B, S = geom
+        H = seq.shape[1]
+        hm = L.gather_rows(seq, pos, S)                                # masked rows, [B*P, H]
+        pre = torch.empty(hm.shape[0], w_t.shape[0], device=hm.device, dtype=hm.dtype)
+        a = torch.empty_like(pre)
+        L.gemm(hm, True, w_t, True, a, 1.0, 0.0, b_t, 2, 0, pre, 3)  # pre := gelu'(hm W^T + b), as in FFN1
+        t, _, mean, rstd = L.ln_fwd(a, None, g, b, eps, 0.0, 0, 0.0, 0, False)
+        logits = gemm(t, True, word, True, bias=dec_bias)
+        loss_rows, _, lse = L.softmax_xent(logits, labels, 1.0 / denom, False)
+        mlm = L.row_sum(loss_rows, 1.0 / denom)
+        cls = seq.view(B, S * H)[:, :H]                                # [CLS] rows, strided (no copy)
+        pooled = gemm(cls, True, pool_w, True, bias=pool_b, act="tanh")
+        total, probs = L.nsp_loss_fwd(pooled, nsp_w, nsp_b, nsp_labels, mlm)
+        ctx.mod_params = holder.params
+        ctx.scale = 1.0 / denom
+        ctx.geom = geom
+        ctx.save_for_backward(seq, pos, hm, pre, a, mean, rstd, t, logits, labels, lse, w_t, g, word, pooled, probs,
+                              nsp_labels, pool_w, nsp_w)
+        return total
+
+    @staticmethod
+    def backward(ctx, gout):
+        L = lib()
+        (seq, pos, hm, pre, a, mean, rstd, t, logits, labels, lse, w_t, g, word, pooled, probs, nsp_labels, pool_w,
+         nsp_w) = ctx.saved_tensors
+        _, _, B, S = ctx.geom
+        H = seq.shape[1]
+        params = ctx.mod_params
+        word_p = params[4]
+        accs = [_gacc(q) for q in params]
+        (gwt, _), (gbt, _), (gg, _), (gb, _), (gword, _), (gdec, _), (gpw, _), (gpb, _), (gnw, _), (gnb, _) = accs
+        gout = gout.float().reshape(1)
+        # masked LM
+        dl = L.softmax_xent_bwd(logits, labels, lse, gout, ctx.scale)
+        L.colsum(dl, gdec, True)
+        gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
+        dt = gemm(dl, True, word, False)
+        da, _ = L.ln_bwd(dt, a, g, mean, rstd, gg, gb, 0.0, 0, 0.0, 0, False)
+        dpre = torch.mul(da, pre)                                      # pre holds gelu'(pre-activation)
+        L.colsum(dpre, gbt, True)
+        gemm(dpre, False, hm, False, out=gwt, beta=1.0)
+        dhm = gemm(dpre, True, w_t, False)
+        # next sentence: dlogits -> (Wn, bn), tanh' -> pooler (Wp, bp) -> [CLS] rows
+        dpp = L.nsp_loss_bwd(pooled, nsp_w, probs, nsp_labels, gout, gnw, gnb)
+        L.colsum(dpp, gpb, True)
+        cls = seq.view(B, S * H)[:, :H]
+        gemm(dpp, False, cls, False, out=gpw, beta=1.0)
+        dcls = gemm(dpp, True, pool_w, False)
+        dseq = torch.empty_like(seq)
+        L.zero_(dseq)
+        L.scatter_rows_add(dseq, pos, dhm, S)
+        L.scatter_rows_add(dseq, None, dcls, S)
+        # the embedding node notifies the shared word-embedding gradient after adding its part
+        grads = _finish(params, accs, skip_notify=(word_p,))
+        return (dseq, None, None, None, None, None, *grads)
+
+
+def heads_loss(model, seq, mlm_positions, mlm_labels, nsp_labels, num_valid, B, S):
+    e = model.emb
+    params = [model.mlm_w, model.mlm_b, model.mlm_ln_g, model.mlm_ln_b, e.word, model.mlm_bias, model.pool_w,
+              model.pool_b, model.nsp_w, model.nsp_b]
+    return _HeadsFn.apply(seq, mlm_positions.contiguous(), mlm_labels.reshape(-1).contiguous(), nsp_labels.contiguous(),
+                          (model.cfg.eps, float(num_valid), B, S), _Holder(params), *params)

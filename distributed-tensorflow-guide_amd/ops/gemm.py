@@ -13,7 +13,7 @@ import torch.nn.functional as F
 from ._native import lib
 from ..parallel import grad_sink
 
-ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "tanh": 3}
 
 
 def gemm(a, a_kc, b, b_kc, out=None, alpha=1.0, beta=0.0, bias=None, act=None, split_k=0, out_dtype=None):

@@ -282,7 +282,7 @@ def test_resnet50_full_network_matches_fp32_reference():
     print("loss %.6f ref %.6f | median grad rel-err: dtg %.4f, fp32 ref under 2^-9 weight noise %.4f, "
           "dtg vs ref without one residual %.4f" % (loss.item(), ref_loss, med(e_dtg.values()), e_noise, e_bad))
     assert abs(loss.item() - ref_loss) < 2e-3 * abs(ref_loss)
-    assert e_dtg["fc.weight"] < 2e-2 and e_dtg["fc.bias"] < 2e-2  # the last layer sees no chaos
+    assert e_dtg["fc.weight"] < 5e-2 and e_dtg["fc.bias"] < 5e-2  # the last layer sees no chaos (bf16 grads)
     assert med(e_dtg.values()) < 1.6 * e_noise + 0.02
     assert max(e_dtg.values()) < 0.7, sorted(e_dtg.items(), key=lambda kv: -kv[1])[:5]
     assert e_bad > 2.0 * med(e_dtg.values())

@@ -302,3 +302,48 @@ def test_pos_embedding_grad_accumulates(B, S, H):
     lib().emb_pos_bwd(ds, gP, S)
     ref = g0.float() + ds.float().view(B, S, H).sum(0)
     assert rel(gP, ref) < 1e-2
+
+
+def test_bert_heads_node_matches_unfused_heads():
+    """bert_fused.heads_loss (gather -> MLM head -> xent, [CLS] -> tanh pooler -> NSP xent, summed, on dtg
+    kernels) equals the previous head path (index_select + mlm_head + F.linear / tanh / F.cross_entropy):
+    loss and every parameter gradient, same fused encoder underneath."""
+    from dtg.models.bert import BertConfig, synthetic_batch
+    cfg = BertConfig(vocab_size=1024, hidden=128, layers=2, heads=2, intermediate=512, max_position=128,
+                     dropout=0.0, attn_dropout=0.0)
+    a, _ = _bert_pair(cfg, seed=1)
+    b, _ = _bert_pair(cfg, seed=1)
+    b.fused_heads = False
+    batch = synthetic_batch(8, 64, cfg, dev, max_predictions=8, seed=4)
+    lab = batch[4].clone()
+    lab[2, 3:] = -1  # some rows without a prediction
+    batch = batch[:4] + (lab,) + batch[5:]
+    la, lb = a(*batch), b(*batch)
+    assert abs(la.item() - lb.item()) < 2e-3 * abs(lb.item()), (la.item(), lb.item())
+    la.backward()
+    lb.backward()
+    worst = sorted(((rel(pa.grad, pb.grad), n) for (n, pa), pb in zip(a.named_parameters(), b.parameters())),
+                   reverse=True)
+    assert worst[0][0] < 2e-2, worst[:5]
+
+
+def test_emb_word_bwd_owned_matches_index_add():
+    """Sort-free word-embedding gradient (heads.hip: vocabulary rows owned per workgroup, token order):
+    equals an fp32 index_add, with a heavily repeated id (more matches than the kernel's list holds, so it
+    flushes mid-scan), ids at both vocabulary ends, and existing gradient contents accumulated."""
+    torch.manual_seed(3)
+    T_, H, V = 6000, 768, 30528
+    ids = torch.randint(0, V, (T_,), device=dev)
+    ids[::3] = 7
+    ids[5] = 0
+    ids[6] = V - 1
+    ds = torch.randn(T_, H, device=dev).bfloat16()
+    g0 = (torch.randn(V, H, device=dev) * 0.1).bfloat16()
+    gw = g0.clone()
+    assert lib().emb_word_bwd_owned(ds, ids, gw)
+    ref = g0.float().index_add(0, ids, ds.float())
+    assert rel(gw, ref) < 1e-2
+    assert rel(gw[7], ref[7]) < 1e-2 and rel(gw[V - 1], ref[V - 1]) < 1e-2
+    gw2 = g0.clone()
+    lib().emb_word_bwd_owned(ds, ids, gw2)
+    assert torch.equal(gw, gw2)  # deterministic
