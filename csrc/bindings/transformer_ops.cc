@@ -263,7 +263,7 @@ Tensor attn_fused_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, c10::opti
   CHECK_GPU_BF16_CONTIG(out);
   CHECK_GPU_BF16_CONTIG(dout);
   CHECK_F32_CONTIG(lse);
-  TORCH_CHECK(dtg::attn_fused_supported((int)S, 64, 1), "fused attention backward: S % 64 == 0 and S <= 128");
+  TORCH_CHECK(dtg::attn_fused_supported((int)S, 64, 1), "fused attention backward: S % 64 == 0 and S <= 512");
   TORCH_CHECK(qkv.size(0) == B * S && qkv.size(1) == 3 * nh * 64, "qkv shape");
   TORCH_CHECK(out.sizes() == dout.sizes() && out.size(0) == B * S && out.size(1) == nh * 64, "out/dout shape");
   TORCH_CHECK(lse.numel() == B * nh * S, "lse size");

@@ -8,7 +8,7 @@
 //   reductions across the 16 lanes that share a row) -> dropout(P) through a per-wave LDS
 //   scratch into A-fragment layout -> O += P V (8 MFMA).  Writes O (bf16, coalesced through LDS) and
 //   LSE = m + log(l) per row for the backward.  No [S, S] matrix ever reaches HBM.
-// Backward (grid: [B*nh], 8 waves; a wave owns 16 keys; S in {64, 128}):
+// Backward (grid: [B*nh], 8 waves; a wave owns 16 keys; S in {64, 128}; longer S: two launches, below):
 //   recomputes P^T = exp(K Q^T * scale + mask - LSE) per 32-query chunk, then
 //   dV += dropout(P)^T dO,  dP^T = V dO^T,  dS^T = P^T (dropout'(dP^T) - D),  dK += dS^T Q * scale;
 //   dS is kept whole in LDS, so after one barrier dQ = dS K * scale is a plain MFMA pass per
@@ -400,6 +400,274 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward at 128 < S <= 512: the whole dS of a head no longer fits LDS (S = 512: 512 KB), so the
+// backward is split in two launches that each recompute P (flash-attention style, no [S, S] tensor
+// in HBM and no atomics):
+//   dKV (grid [B*nh, S/128], 8 waves, wave w owns keys 128*y + 16w + [0, 16)): phase 1 of the
+//       kernel above over all S queries in 32-query chunks; dropout(P)^T and dS^T go through two
+//       per-wave [32 q][16 key] scratches instead of the head's dS matrix.
+//   dQ  (grid [B*nh, S/128], 8 waves, wave w owns queries 128*y + 16w + [0, 16)): K and V of the
+//       head staged once as KC tiles (the forward's layout); per 64-key chunk S = Q K^T and
+//       dP = dO V^T (16 MFMA), dS = P (dropout'(dP) - D) into the wave's [16 q][64 key] KC scratch,
+//       dQ += dS K (8 MFMA) with K read TRANSPOSED out of its KC image (frag_tr_kc).
+// LDS at S = 512: dKV 148 KB (Q, dO MC tiles), dQ 146 KB (K, V KC tiles): one workgroup per CU.
+
+// B fragment X_B[n][k] = T[k][n] of a KC image T [rows = k][64 cols = n] (frag_kc's swizzle): the
+// MC-orientation read of a tile that was staged row-wise (ds_read_b64_tr_b16, 4 rows x 4 cols per lane
+// address; the chunk XOR moves whole 16-B chunks, so each 8-byte half stays contiguous)
+__device__ __forceinline__ v8bf frag_tr_kc(const lds_char* t, int n0, int ks, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int kA = ks * 32 + 8 * g + q, kB = kA + 4;
+  const int ch = (n0 + 4 * p) >> 3, sub = (p & 1) * 8;
+  const lds_char* a = t + kA * 128 + ((ch ^ (kA & 7)) << 4) + sub;
+  const lds_char* b = t + kB * 128 + ((ch ^ (kB & 7)) << 4) + sub;
+  const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(a));
+  const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(b));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+constexpr int kLongKeys = 128;  // keys (dKV) / queries (dQ) per workgroup of the long backward
+
+__global__ void __launch_bounds__(512) attn_bwd_dkv_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                           const bf16_t* __restrict__ dout,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
+                                                           int S, int nh, float scale, uint32_t th, float dscale,
+                                                           uint32_t seed) {
+  constexpr int NW = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int H = nh * 64;
+  const long long ld = 3LL * H;
+  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bf16_t* Qg = qkv + (long long)b * S * ld + h * 64;
+  const bf16_t* Kg = Qg + H;
+  const bf16_t* Vg = Qg + 2 * H;
+  const bf16_t* Og = o + (long long)b * S * H + h * 64;
+  const bf16_t* dOg = dout + (long long)b * S * H + h * 64;
+  lds_char* Qt = smem;                          // S/64 MC tiles [64 q][64 d]
+  lds_char* dOt = Qt + S * 128;                 // same for dO; after the loop: per-wave output staging
+  lds_float* Ds = reinterpret_cast<lds_float*>(dOt + S * 128);
+  lds_float* Ls = Ds + S;
+  lds_char* scr = reinterpret_cast<lds_char*>(Ls + S) + wave * 2048;  // [32 q][16 keys] x {P, dS}
+  const int kb = blockIdx.y * kLongKeys + wave * 16;
+  const bool has_keys = kb < S;  // wave-uniform
+  const int rbase = (lane >> 4) * 4;
+  constexpr float kLog2e = 1.4426950408889634f;
+  float msl[4] = {0.f, 0.f, 0.f, 0.f};
+  if (has_keys && mask) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) msl[r] = mask[(long long)b * S + kb + rbase + r] * kLog2e;
+  }
+  {
+    DenseMC<false> qs_{Qg, ld, 64, S};
+    DenseMC<false> ds_{dOg, (long long)H, 64, S};
+    for (int c = 0; c < S / 64; ++c) {
+      stage_mc<64, DenseMC<false>, NW>(qs_, Qt + c * 8192, 0, c * 64, wave, lane);
+      stage_mc<64, DenseMC<false>, NW>(ds_, dOt + c * 8192, 0, c * 64, wave, lane);
+    }
+  }
+  for (int i = tid; i < 2 * S; i += 64 * NW) {  // D[q] = sum_d dO[q, d] * O[q, d]: two threads per row
+    const int q = i >> 1, half = i & 1;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float a[8], bb[8];
+      load8_bf16(dOg + (long long)q * H + half * 32 + c * 8, a);
+      load8_bf16(Og + (long long)q * H + half * 32 + c * 8, bb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += a[k] * bb[k];
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    if (half == 0) Ds[q] = acc;
+  }
+  for (int i = tid; i < S; i += 64 * NW) Ls[i] = lse[(long long)bh * S + i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 dk[4], dv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dk[j] = dv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (has_keys) {
+    const float sl2 = scale * kLog2e;
+    const v8bf ka0 = gfrag(Kg, ld, kb, 0, lane), ka1 = gfrag(Kg, ld, kb, 1, lane);
+    const v8bf va0 = gfrag(Vg, ld, kb, 0, lane), va1 = gfrag(Vg, ld, kb, 1, lane);
+    lds_char* scp = scr;
+    lds_char* scs = scr + 1024;
+#pragma unroll 1
+    for (int qc = 0; qc < S; qc += 32) {
+      const int tq = qc >> 6, kq = (qc & 63) >> 5;
+      f32x4 st[2], dpt[2];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int qrow = (qc & 63) + ni * 16 + (lane & 15), cb = lane >> 4;
+        const int sw = mc_swz<8>(qrow);
+        const lds_char* qt = Qt + tq * 8192 + qrow * 128;
+        const lds_char* dt = dOt + tq * 8192 + qrow * 128;
+        const v8bf qb0 = *reinterpret_cast<const lds_v8bf*>(qt + ((cb ^ sw) << 4));
+        const v8bf qb1 = *reinterpret_cast<const lds_v8bf*>(qt + (((4 + cb) ^ sw) << 4));
+        const v8bf db0 = *reinterpret_cast<const lds_v8bf*>(dt + ((cb ^ sw) << 4));
+        const v8bf db1 = *reinterpret_cast<const lds_v8bf*>(dt + (((4 + cb) ^ sw) << 4));
+        f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka0, qb0, z, 0, 0, 0);
+        st[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka1, qb1, z, 0, 0, 0);
+        z = f32x4{0.f, 0.f, 0.f, 0.f};
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va0, db0, z, 0, 0, 0);
+        dpt[ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va1, db1, z, 0, 0, 0);
+      }
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int ql = ni * 16 + (lane & 15), q = qc + ql;
+        const float lq = Ls[q] * kLog2e, dq = Ds[q];
+        const uint32_t ib = ((uint32_t)bh * (uint32_t)S + (uint32_t)q) * (uint32_t)S + (uint32_t)(kb + rbase);
+        float pd[4], dsv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], sl2, msl[r] - lq));
+          float pv = p, dp = dpt[ni][r];
+          if (th) {
+            const bool kp = keep_elem(seed, ib + r, th);
+            pv = kp ? p * dscale : 0.f;
+            dp = kp ? dp * dscale : 0.f;
+          }
+          pd[r] = pv;
+          dsv[r] = p * (dp - dq);
+        }
+        st4_bf16(scp + ql * 32 + rbase * 2, pd);
+        st4_bf16(scs + ql * 32 + rbase * 2, dsv);
+      }
+      lds_fence();
+      const v8bf pa = frag_mc<16>(scp, 0, 0, lane);  // dropout(P)^T [16 keys][32 q]
+      const v8bf sa = frag_mc<16>(scs, 0, 0, lane);  // dS^T [16 keys][32 q]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dv[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_mc<64>(dOt + tq * 8192, j * 16, kq, lane), dv[j], 0,
+                                                        0, 0);
+        dk[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, frag_mc<64>(Qt + tq * 8192, j * 16, kq, lane), dk[j], 0,
+                                                        0, 0);
+      }
+      lds_fence();  // scratches rewritten by the next chunk
+    }
+  }
+  __syncthreads();  // every wave is done with the Q / dO tiles
+  if (has_keys) {
+    lds_char* stg = dOt + wave * 2048;
+    bf16_t* gk = dqkv + ((long long)b * S + kb) * ld + H + h * 64;
+    store_rows16(stg, dk, scale, gk, ld, lane);
+    store_rows16(stg, dv, 1.f, gk + H, ld, lane);
+  }
+}
+
+__global__ void __launch_bounds__(512) attn_bwd_dq_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
+                                                          const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+                                                          const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
+                                                          int S, int nh, float scale, uint32_t th, float dscale,
+                                                          uint32_t seed) {
+  constexpr int NW = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int H = nh * 64;
+  const long long ld = 3LL * H;
+  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bf16_t* Qg = qkv + (long long)b * S * ld + h * 64;
+  const bf16_t* Kg = Qg + H;
+  const bf16_t* Vg = Qg + 2 * H;
+  const bf16_t* Og = o + (long long)b * S * H + h * 64;
+  const bf16_t* dOg = dout + (long long)b * S * H + h * 64;
+  lds_char* Kt = smem;                        // S/64 KC tiles [64 keys][64 d]
+  lds_char* Vt = smem + S * 128;              // same for V
+  lds_float* Mk = reinterpret_cast<lds_float*>(smem + 2 * S * 128);
+  lds_char* scr = reinterpret_cast<lds_char*>(Mk + S) + wave * 2048;  // dS [16 q][64 keys] KC
+  {
+    DenseKC<false> ks_{Kg, ld, S, 64};
+    DenseKC<false> vs_{Vg, ld, S, 64};
+    for (int c = 0; c < S / 64; ++c) {
+      stage_kc<64, DenseKC<false>, NW>(ks_, Kt + c * 8192, c * 64, 0, wave, lane);
+      stage_kc<64, DenseKC<false>, NW>(vs_, Vt + c * 8192, c * 64, 0, wave, lane);
+    }
+  }
+  constexpr float kLog2e = 1.4426950408889634f;
+  for (int i = tid; i < S; i += 64 * NW) Mk[i] = mask ? mask[(long long)b * S + i] * kLog2e : 0.f;
+  const int q0 = blockIdx.y * kLongKeys + wave * 16;
+  const bool active = q0 < S;  // wave-uniform
+  const int rbase = (lane >> 4) * 4;
+  v8bf qa[2], da[2];
+  float lq[4], dd[4];
+  if (active) {
+    qa[0] = gfrag(Qg, ld, q0, 0, lane);
+    qa[1] = gfrag(Qg, ld, q0, 1, lane);
+    da[0] = gfrag(dOg, (long long)H, q0, 0, lane);
+    da[1] = gfrag(dOg, (long long)H, q0, 1, lane);
+    // D of the wave's 16 rows: 4 lanes per row, 16 d each
+    const int row = lane >> 2, part = lane & 3;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      float a[8], bb[8];
+      load8_bf16(dOg + (long long)(q0 + row) * H + part * 16 + c * 8, a);
+      load8_bf16(Og + (long long)(q0 + row) * H + part * 16 + c * 8, bb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += a[k] * bb[k];
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dd[r] = __shfl(acc, (rbase + r) * 4, 64);
+      lq[r] = lse[(long long)bh * S + q0 + rbase + r] * kLog2e;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (!active) return;  // (no barrier below this point)
+  const float sl2 = scale * kLog2e;
+  f32x4 dq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dq[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kc = 0; kc < S / 64; ++kc) {
+    const lds_char* kt = Kt + kc * 8192;
+    const lds_char* vt = Vt + kc * 8192;
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], frag_kc(kt, j * 16, ks, lane), s[j], 0, 0, 0);
+        dp[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[ks], frag_kc(vt, j * 16, ks, lane), dp[j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = kc * 64 + j * 16 + (lane & 15);
+      const float mk = Mk[key];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[j][r], sl2, mk - lq[r]));
+        float dpv = dp[j][r];
+        if (th) {
+          const uint32_t idx = ((uint32_t)bh * (uint32_t)S + (uint32_t)(q0 + rbase + r)) * (uint32_t)S + (uint32_t)key;
+          dpv = keep_elem(seed, idx, th) ? dpv * dscale : 0.f;
+        }
+        st_bf16(scr, kc_off(rbase + r, j * 16 + (lane & 15)), p * (dpv - dd[r]));
+      }
+    }
+    lds_fence();
+    const v8bf a0 = frag_kc(scr, 0, 0, lane), a1 = frag_kc(scr, 0, 1, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, frag_tr_kc(kt, j * 16, 0, lane), dq[j], 0, 0, 0);
+      dq[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, frag_tr_kc(kt, j * 16, 1, lane), dq[j], 0, 0, 0);
+    }
+    lds_fence();  // the scratch is rewritten by the next chunk
+  }
+  store_rows16(scr, dq, scale, dqkv + ((long long)b * S + q0) * ld + h * 64, ld, lane);
+}
+
 static uint32_t drop_th(float p) {
   if (p <= 0.f) return 0u;
   const double t = (double)p * 4294967296.0;
@@ -408,11 +676,13 @@ static uint32_t drop_th(float p) {
 
 int attn_fused_supported(int S, int dh, int backward) {
   if (dh != 64 || S % 64 != 0 || S <= 0) return 0;
-  return backward ? (S == 64 || S == 128) : (S <= 512);
+  return S <= 512;  // backward: the one-launch kernel at S <= 128, the dKV + dQ pair above that
 }
 
 static size_t fwd_lds(int S) { return (size_t)2 * S * 128 + kFwdWaves * 2048 + (size_t)S * 4; }
 static size_t bwd_lds(int S) { return (size_t)2 * S * 128 + (size_t)S * S * 2 + 3 * S * 4 + 8 * 1024; }
+static size_t dkv_lds(int S) { return (size_t)2 * S * 128 + (size_t)2 * S * 4 + 8 * 2048; }
+static size_t dq_lds(int S) { return (size_t)2 * S * 128 + (size_t)S * 4 + 8 * 2048; }
 
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,
               uint32_t seed, hipStream_t st) {
@@ -437,9 +707,19 @@ void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const floa
   if (!attr) {
     DTG_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_kernel<128>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds(128)));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)dkv_lds(512)));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)dq_lds(512)));
     attr = true;
   }
-  if (S == 64)
+  if (S > 128) {
+    const dim3 grid(B * nh, (S + kLongKeys - 1) / kLongKeys);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(512), dkv_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
+                       0.125f, th, ds, seed);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(512), dq_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
+                       0.125f, th, ds, seed);
+  } else if (S == 64)
     hipLaunchKernelGGL(attn_bwd_kernel<64>, dim3(B * nh), dim3(512), bwd_lds(64), st, qkv, o, dout, lse, mask, dqkv,
                        nh, 0.125f, th, ds, seed);
   else

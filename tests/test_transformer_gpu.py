@@ -238,7 +238,7 @@ def test_bert_flat_adam_trains():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
-@pytest.mark.parametrize("S", [64, 128])
+@pytest.mark.parametrize("S", [64, 128, 192, 256, 512])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_fused_attention_fwd_bwd(S, p):
     torch.manual_seed(6)
