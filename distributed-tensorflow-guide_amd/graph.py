@@ -52,6 +52,7 @@ class Graph:
         self._name_stack = []
         self._lock = threading.RLock()
         self.servers = []
+        self._nodes = []  # every node in creation order (as_graph_def / write_graph)
 
     def unique_name(self, base, mark_used=True):
         scope = "/".join(self._name_stack)
@@ -111,6 +112,13 @@ class Graph:
     def current_device(self, node=None):
         from .placement import resolve_device
         return resolve_device(self._device_stack, node)
+
+    def get_operations(self):
+        return list(self._nodes)
+
+    def as_graph_def(self, add_shapes=False):
+        """The graph as a TF ``GraphDef`` (text-proto serialisable, ``str(graph_def)``)."""
+        return GraphDef(self._nodes, add_shapes)
 
 
 _default = Graph()
@@ -224,6 +232,8 @@ class Node:
         self.inputs = list(inputs)
         self.control_inputs = g.current_control_inputs()
         self.device = g.current_device(self)
+        self.op_type = _op_type(name or kind, kind)
+        g._nodes.append(self)
 
     # TF-compat: t.name == 'add:0', t.op.name == 'add'
     @property
@@ -245,6 +255,77 @@ class Node:
         return f"<dtg.{type(self).__name__} '{self.name}' device={self.device}>"
 
     __hash__ = object.__hash__
+
+
+# TF op type of a node, from the base name its constructor was given (graph.pbtxt)
+_OP_TYPES = {"add": "Add", "sub": "Sub", "mul": "Mul", "truediv": "RealDiv", "pow": "Pow", "strided_slice": "StridedSlice",
+             "group_deps": "NoOp", "init": "NoOp", "init_1": "NoOp", "Op": "NoOp", "Tensor": "Identity",
+             "Variable": "VariableV2"}
+
+
+def _op_type(base, kind):
+    if kind == "Variable":
+        return "VariableV2"
+    b = base.rsplit("/", 1)[-1]
+    if b in _OP_TYPES:
+        return _OP_TYPES[b]
+    return "".join(p[:1].upper() + p[1:] for p in b.split("_") if p) or "NoOp"
+
+
+def _tf_dtype(dt):
+    return {torch.float32: "DT_FLOAT", torch.float64: "DT_DOUBLE", torch.int32: "DT_INT32", torch.int64: "DT_INT64",
+            torch.bfloat16: "DT_BFLOAT16", torch.float16: "DT_HALF", torch.bool: "DT_BOOL"}.get(dt, "DT_FLOAT")
+
+
+def _q(s):
+    return '"' + str(s).replace("\\", "\\\\").replace('"', '\\"') + '"'
+
+
+class GraphDef:
+    """``tf.GraphDef`` of a dtg graph: one ``node`` per graph node (name, TF op type, data inputs, ``^control``
+    inputs, device; dtype/shape attrs on variables).  ``str()`` is the text proto TF writes as graph.pbtxt
+    (DOWNPOUR/DOWNPOUR.py:121-127 gets one from MonitoredTrainingSession's checkpoint_dir)."""
+
+    def __init__(self, nodes, add_shapes=False):
+        self.node = list(nodes)
+        self.add_shapes = add_shapes
+
+    def _node_text(self, n):
+        lines = ["node {", f"  name: {_q(n._name)}", f"  op: {_q(n.op_type)}"]
+        for i in n.inputs:
+            if isinstance(i, Node):
+                lines.append(f"  input: {_q(i._name)}")
+        for c in n.control_inputs:
+            if isinstance(c, Node):
+                lines.append(f"  input: {_q('^' + c._name)}")
+        dev = n.device.to_string() if getattr(n, "device", None) is not None else ""
+        if dev:
+            lines.append(f"  device: {_q(dev)}")
+        if getattr(n, "_is_variable", False):
+            dims = " ".join(f"dim {{ size: {int(d)} }}" for d in n.shape)
+            lines.append(f"  attr {{ key: \"dtype\" value {{ type: {_tf_dtype(n.dtype)} }} }}")
+            lines.append(f"  attr {{ key: \"shape\" value {{ shape {{ {dims} }} }} }}")
+        lines.append("}")
+        return "\n".join(lines)
+
+    def __str__(self):
+        return "\n".join([self._node_text(n) for n in self.node] + ["versions {", "  producer: 24", "}"]) + "\n"
+
+    def SerializeToString(self):  # noqa: N802 - tf name (text form; TF's binary proto is not reproduced)
+        return str(self).encode()
+
+
+def write_graph(graph_or_graph_def, logdir, name, as_text=True):
+    """tf.train.write_graph: <logdir>/<name> as a GraphDef text proto."""
+    import os
+    gd = graph_or_graph_def.as_graph_def() if isinstance(graph_or_graph_def, Graph) else graph_or_graph_def
+    os.makedirs(logdir, exist_ok=True)
+    path = os.path.join(logdir, name)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(str(gd))
+    os.replace(tmp, path)
+    return path
 
 
 class _NodeOpRef:

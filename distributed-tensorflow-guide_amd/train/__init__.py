@@ -29,3 +29,4 @@ def barrier(name, count=None, timeout=600.0, ps_task=0):
         return True
     n = count if count is not None else s.cluster.num_tasks("worker")
     return client_for("ps", ps_task).barrier(name, int(n), float(timeout))
+from ..graph import write_graph  # noqa: F401,E402  (tf.train.write_graph)

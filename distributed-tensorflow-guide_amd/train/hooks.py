@@ -208,6 +208,9 @@ class CheckpointSaverHook(SessionRunHook):
         self._gs = _gs_var()
 
     def after_create_session(self, session, coord):
+        from .. import graph as G
+        # TF's CheckpointSaverHook writes the graph next to the checkpoints (graph.pbtxt)
+        G.write_graph(G.get_default_graph(), self._dir, "graph.pbtxt")
         self._last_t = time.time()
         step = int(session._read(self._gs)) if self._gs is not None else 0
         self._save(session, step)  # TF saves the initial state too

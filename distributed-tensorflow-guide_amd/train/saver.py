@@ -3,8 +3,11 @@
     <dir>/checkpoint                          CheckpointState text proto (max_to_keep = 5)
     <dir>/model.ckpt-<N>.index                TensorBundle SSTable  } written by the native
     <dir>/model.ckpt-<N>.data-00000-of-00001  raw tensor bytes      } writer (csrc/ckpt)
-    <dir>/model.ckpt-<N>.meta                 dtg graph manifest (JSON; TF's MetaGraphDef is not
+    <dir>/model.ckpt-<N>.meta                 dtg graph manifest (JSON; TF's binary MetaGraphDef is not
                                               reproduced -- SURVEY §7.5 item 5 open decision)
+    <dir>/graph.pbtxt                         GraphDef text proto of the default graph (node name, op type,
+                                              inputs, ^control inputs, device, variable dtype/shape), written
+                                              by CheckpointSaverHook / Supervisor like TF (dtg.graph.GraphDef)
 
 Keys are variable op names (``Variable``, ``Variable_1``, ``global_step``, ``g/Variable``, ...),
 plus the optimizer slots the parameter servers created (``g/Variable/Adagrad``).  Local variables

@@ -384,6 +384,8 @@ class Supervisor:
         if self.is_chief:
             if self.logdir:
                 os.makedirs(self.logdir, exist_ok=True)
+                from .. import graph as G
+                G.write_graph(G.get_default_graph(), self.logdir, "graph.pbtxt")  # Supervisor._write_graph
             self._sm.prepare_session(sess, self.init_op, self.saver, self.logdir, self.init_fn, self.init_feed_dict)
             if start_standard_services and self.logdir and self.save_model_secs and self.save_model_secs > 0:
                 self._saver_thread = threading.Thread(target=self._save_loop, daemon=True, name="sv_saver")

@@ -30,6 +30,10 @@ def test_downpour_one_worker_oracle(tmp_path):
     keys = dtg.train.NewCheckpointReader(ck).get_variable_to_shape_map()
     assert {"global_step", "g/Variable", "g/Variable_1", "g/Variable/Adagrad", "g/Variable_1/Adagrad"} <= set(keys)
     assert "Variable" not in keys and "local_step" not in keys  # local variables are not saved
+    # graph.pbtxt next to the checkpoints (TF's CheckpointSaverHook): the chief's GraphDef text proto
+    gp = (tmp_path / "logdir" / "graph.pbtxt").read_text()
+    assert 'name: "global_step"' in gp and 'op: "VariableV2"' in gp and gp.rstrip().endswith("}")
+    assert 'name: "g/Variable"' in gp and 'device: "/job:ps/task:0' in gp
 
 
 def test_downpour_resume_stops_immediately(tmp_path):
@@ -138,6 +142,7 @@ def test_distributed_setup_supervisor(tmp_path):
     out = run_cluster("Distributed-Setup/dist_setup_sup.py", 1, 1, ["--steps", "50", "--logdir", str(tmp_path / "l")])
     _ok(out)
     assert os.path.exists(tmp_path / "l" / "checkpoint")
+    assert 'op: "VariableV2"' in (tmp_path / "l" / "graph.pbtxt").read_text()  # Supervisor writes the graph
 
 
 def test_multi_gpu_example_runs_on_cpu(tmp_path):

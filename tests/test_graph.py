@@ -135,3 +135,23 @@ def test_hooks_surface():
         sess.run(train)
     sess.close()
     assert final.final_ops_values is not None and counter.history and "examples/sec" in counter.history[-1]
+
+
+def test_graph_def_text_proto(tmp_path):
+    import dtg
+    from dtg import graph as G
+    G.reset_default_graph()
+    with dtg.device("/job:ps/task:0"):
+        a = dtg.Variable([1.0, 2.0], name="a")
+    with dtg.device("/job:worker/task:0"):
+        b = dtg.constant(3.0)
+        with dtg.control_dependencies([a.initializer]):
+            c = a * b
+    gd = G.get_default_graph().as_graph_def()
+    txt = str(gd)
+    assert 'name: "a"\n  op: "VariableV2"' in txt and "dim { size: 2 }" in txt and 'device: "/job:ps/task:0"' in txt
+    assert 'name: "mul"\n  op: "Mul"\n  input: "a"\n  input: "Const"\n  input: "^a/Assign"' in txt
+    path = dtg.train.write_graph(gd, str(tmp_path), "graph.pbtxt")
+    assert open(path).read() == txt and txt.endswith("versions {\n  producer: 24\n}\n")
+    assert [n.name for n in G.get_default_graph().get_operations()][:2] == ["a:0", "Const:0"]
+    G.reset_default_graph()

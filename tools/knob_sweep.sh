@@ -14,6 +14,15 @@ if [ "$model" = resnet ]; then
   run DTG_WGRAD_BLOCKS=2048
   run DTG_BN_BITS=0
   run X=0
+elif [ "$model" = bert_wgrad ]; then  # weight-gradient placement / split-K knobs of the BERT step
+  model=bert
+  run X=0
+  run DTG_WGRAD_STREAM=0
+  run DTG_GEMM_SPLIT_WGS=256
+  run DTG_GEMM_SPLIT_WGS=1024
+  run DTG_SIDE_PRIO=0
+  run DTG_WGRAD_STREAM=0 DTG_GEMM_SPLIT_WGS=256
+  run X=0
 else
   run X=0
   run DTG_LN_BWD_BLOCKS=1024
