@@ -1,6 +1,7 @@
 // BatchNorm host geometry (rows x channel-slab decomposition) and the statistics finalize kernel,
 // shared by batchnorm.hip and the fused stem kernels (stem.hip).
 #pragma once
+#include <stdlib.h>
 #include "dtg/common.h"
 
 namespace dtg {
@@ -33,11 +34,17 @@ inline BnGeom bn_geom(long long M, int C) {
   return g;
 }
 
-// The elementwise passes (apply, dx) write no partials, so they run on a much larger grid than the
-// reductions (whose partial count the finalize kernel bounds): ~2048 workgroups.
+// The elementwise passes (apply, dx) write no partials, so their grid is free: each workgroup takes
+// 2 x RPP rows, i.e. every thread streams exactly two rows of its 8 channels (all loads in flight, then the
+// stores) and exits.  Measured against the previous ~2048 long-running workgroups (tools/bn_bench.py,
+// profiles/r03_bn_grid): ResNet-50's largest apply+residual pass 5.0 -> 5.7 TB/s, its dx pass 5.1 -> 6.2
+// TB/s, i.e. the 6.0 TB/s of a plain torch.add moving the same bytes.  DTG_BN_EWG=<workgroups> restores
+// the fixed-count grid for A/B runs.
 inline long long elementwise_rpc(const BnGeom& g, long long M) {
   const int rpp = kBlk / g.tpr;
-  long long nc = 2048 / g.gy;
+  static const long long wgs = getenv("DTG_BN_EWG") ? atoll(getenv("DTG_BN_EWG")) : 0;
+  if (wgs <= 0) return 2LL * rpp;
+  long long nc = wgs / g.gy;
   const long long max_chunks = (M + rpp - 1) / rpp;
   if (nc > max_chunks) nc = max_chunks;
   if (nc < 1) nc = 1;

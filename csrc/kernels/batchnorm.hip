@@ -73,7 +73,24 @@ __device__ __forceinline__ uint8_t pos_bits8(const float (&v)[8]) {
   return (uint8_t)b;
 }
 
-template <int TPR, bool RES, bool RELU>
+// packed relu-mask byte of this lane's 8 channels -> bits[off >> 3].  The 4 lanes tx = 4i .. 4i+3 of a row
+// hold 4 consecutive bytes: with C % 32 == 0 they are gathered by two lane shuffles into one 4-byte store by
+// the first of them (a byte store per lane measured ~1/5 of the apply pass's bandwidth lost)
+__device__ __forceinline__ void store_bits(uint8_t* bits, long long off, const float (&v)[8], int tx, int C) {
+  const uint32_t b = pos_bits8(v);
+  if ((C & 31) == 0) {
+    uint32_t w = b << (8 * (tx & 3));
+    w |= __shfl_xor(w, 1, 64);
+    w |= __shfl_xor(w, 2, 64);
+    if ((tx & 3) == 0) *reinterpret_cast<uint32_t*>(bits + (off >> 3)) = w;
+  } else {
+    bits[off >> 3] = (uint8_t)b;
+  }
+}
+
+// RU rows per loop iteration, all their loads issued before any math (the launcher picks RU = 2 with one
+// iteration per thread: elementwise_rpc)
+template <int TPR, bool RES, bool RELU, int RU = 4>
 __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                         bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                         long long M, int C, long long rpc,
@@ -96,23 +113,20 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
       a[k] = v;
     }
     store8_bf16(y + off, a);
-    if (bits) bits[off >> 3] = pos_bits8(a);  // off = m*C + c0, both multiples of 8
+    if (bits) store_bits(bits, off, a, tx, C);  // off = m*C + c0, both multiples of 8
   };
   long long m = m0 + ty;
-  // 2 rows per iteration: all four 16-B loads are in flight before any math (memory-level parallelism)
-  for (; m + RPP < m1; m += 2 * RPP) {
-    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
-    float a0[8], a1[8], r0[8], r1[8];
-    load8_bf16(x + o0, a0);
-    load8_bf16(x + o1, a1);
-    if constexpr (RES) {
-      load8_bf16(res + o0, r0);
-      load8_bf16(res + o1, r1);
+  for (; m + (RU - 1) * RPP < m1; m += RU * RPP) {  // RU rows per iteration: every load in flight before any math
+    float a[RU][8], r[RU][8];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      load8_bf16(x + (m + u * RPP) * C + c0, a[u]);
+      if constexpr (RES) load8_bf16(res + (m + u * RPP) * C + c0, r[u]);
     }
-    finish(a0, r0, o0);
-    finish(a1, r1, o1);
+#pragma unroll
+    for (int u = 0; u < RU; ++u) finish(a[u], r[u], (m + u * RPP) * C + c0);
   }
-  if (m < m1) {
+  for (; m < m1; m += RPP) {
     const long long o0 = m * C + c0;
     float a0[8], r0[8];
     load8_bf16(x + o0, a0);
@@ -122,7 +136,7 @@ __global__ void __launch_bounds__(kBlk) bn_apply_kernel(const bf16_t* __restrict
 }
 
 // ---- fwd, projection blocks: out = relu(bn3(x) + bn_d(r)), both BNs applied in one pass ---------
-template <int TPR>
+template <int TPR, int RU = 4>
 __global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
                                                          bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                          const float* __restrict__ coef2, long long M, int C,
@@ -140,35 +154,29 @@ __global__ void __launch_bounds__(kBlk) bn_apply2_kernel(const bf16_t* __restric
   for (int k = 0; k < 8; ++k) sf[k] += sf2[k];
   const long long m0 = (long long)blockIdx.x * rpc;
   const long long m1 = m0 + rpc < M ? m0 + rpc : M;
-  long long m = m0 + ty;
-  for (; m + RPP < m1; m += 2 * RPP) {
-    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
-    float a0[8], a1[8], b0[8], b1[8];
-    load8_bf16(x + o0, a0);
-    load8_bf16(x + o1, a1);
-    load8_bf16(r + o0, b0);
-    load8_bf16(r + o1, b1);
+  auto finish = [&](float (&a)[8], const float (&b)[8], long long o) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      a0[k] = fmaxf(fmaf(a0[k], sc[k], fmaf(b0[k], sc2[k], sf[k])), 0.f);
-      a1[k] = fmaxf(fmaf(a1[k], sc[k], fmaf(b1[k], sc2[k], sf[k])), 0.f);
+    for (int k = 0; k < 8; ++k) a[k] = fmaxf(fmaf(a[k], sc[k], fmaf(b[k], sc2[k], sf[k])), 0.f);
+    store8_bf16(y + o, a);
+    if (bits) store_bits(bits, o, a, tx, C);
+  };
+  long long m = m0 + ty;
+  for (; m + (RU - 1) * RPP < m1; m += RU * RPP) {
+    float a[RU][8], b[RU][8];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      load8_bf16(x + (m + u * RPP) * C + c0, a[u]);
+      load8_bf16(r + (m + u * RPP) * C + c0, b[u]);
     }
-    store8_bf16(y + o0, a0);
-    store8_bf16(y + o1, a1);
-    if (bits) {
-      bits[o0 >> 3] = pos_bits8(a0);
-      bits[o1 >> 3] = pos_bits8(a1);
-    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) finish(a[u], b[u], (m + u * RPP) * C + c0);
   }
-  if (m < m1) {
+  for (; m < m1; m += RPP) {
     const long long o0 = m * C + c0;
     float a0[8], b0[8];
     load8_bf16(x + o0, a0);
     load8_bf16(r + o0, b0);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a0[k] = fmaxf(fmaf(a0[k], sc[k], fmaf(b0[k], sc2[k], sf[k])), 0.f);
-    store8_bf16(y + o0, a0);
-    if (bits) bits[o0 >> 3] = pos_bits8(a0);
+    finish(a0, b0, o0);
   }
 }
 
@@ -239,7 +247,7 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_reduce_kernel(const bf16_t* __res
 }
 
 // ---- pass 2 (bwd): dx = a*dp + bx*x + c0 ; dres = dp ------------------------------------------
-template <int TPR, bool RELU, bool DRES, bool NT = true>
+template <int TPR, bool RELU, bool DRES, bool NT = true, int RU = 4>
 __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                          const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
@@ -265,44 +273,43 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
     for (int k = 0; k < 8; ++k) o[k] = a[k] * g[k] + bx[k] * xv[k] + cc[k];
     store8_bf16(dx + off, o);
   };
+  // dp and the saved BN input are read for the last time in this step: non-temporal, so the dx written
+  // here stays cached for the dgrad / wgrad GEMMs that read it next
+  auto ld = [&](const bf16_t* p, float (&v)[8]) {
+    if constexpr (NT) load8_bf16_nt(p, v);
+    else load8_bf16(p, v);
+  };
   long long m = m0 + ty;
-  for (; m + RPP < m1; m += 2 * RPP) {  // 2 rows per iteration, up to six 16-B loads in flight
-    const long long o0 = m * C + c0, o1 = (m + RPP) * C + c0;
-    float g0[8], g1[8], x0[8], x1[8], y0[8], y1[8];
-    // dp and the saved BN input are read for the last time in this step: non-temporal, so the dx written
-    // here stays cached for the dgrad / wgrad GEMMs that read it next
-    if constexpr (NT) {
-      load8_bf16_nt(dy + o0, g0);
-      load8_bf16_nt(dy + o1, g1);
-      load8_bf16_nt(x + o0, x0);
-      load8_bf16_nt(x + o1, x1);
-    } else {
-      load8_bf16(dy + o0, g0);
-      load8_bf16(dy + o1, g1);
-      load8_bf16(x + o0, x0);
-      load8_bf16(x + o1, x1);
+  for (; m + (RU - 1) * RPP < m1; m += RU * RPP) {  // RU rows per iteration, every load in flight first
+    float g[RU][8], xv[RU][8], yv[RU][8];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const long long o = (m + u * RPP) * C + c0;
+      ld(dy + o, g[u]);
+      ld(x + o, xv[u]);
+      if constexpr (RELU) load8_bf16(y + o, yv[u]);
     }
-    if constexpr (RELU) {
-      load8_bf16(y + o0, y0);
-      load8_bf16(y + o1, y1);
-    }
-    finish(g0, x0, y0, o0);
-    finish(g1, x1, y1, o1);
+#pragma unroll
+    for (int u = 0; u < RU; ++u) finish(g[u], xv[u], yv[u], (m + u * RPP) * C + c0);
   }
-  if (m < m1) {
+  for (; m < m1; m += RPP) {
     const long long o0 = m * C + c0;
     float g0[8], x0[8], y0[8];
-    if constexpr (NT) {
-      load8_bf16_nt(dy + o0, g0);
-      load8_bf16_nt(x + o0, x0);
-    } else {
-      load8_bf16(dy + o0, g0);
-      load8_bf16(x + o0, x0);
-    }
+    ld(dy + o0, g0);
+    ld(x + o0, x0);
     if constexpr (RELU) load8_bf16(y + o0, y0);
     finish(g0, x0, y0, o0);
   }
 }
+
+static int bn_ru() {  // rows per loop iteration of the streaming passes (2 = one iteration per thread, see
+                     // elementwise_rpc; DTG_BN_RU=4 for A/B runs with DTG_BN_EWG)
+  static const int ru = getenv("DTG_BN_RU") && atoi(getenv("DTG_BN_RU")) == 4 ? 4 : 2;
+  return ru;
+}
+#define DTG_RU_SWITCH(...)                                 \
+  if (bn_ru() == 2) { constexpr int RU = 2; __VA_ARGS__; } \
+  else { constexpr int RU = 4; __VA_ARGS__; }
 
 static bool bn_nt_loads() {
   static const bool on = !getenv("DTG_BN_NT") || atoi(getenv("DTG_BN_NT")) != 0;
@@ -314,15 +321,15 @@ static void bn_apply_launch(const BnGeom& g, const bf16_t* x, const bf16_t* res,
                             long long M, int C, int relu, hipStream_t st, uint8_t* bits = nullptr) {
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
-  DTG_TPR_SWITCH(g.tpr, {
+  DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
-      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      if (relu) bn_apply_kernel<T, true, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      else bn_apply_kernel<T, true, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
     } else {
-      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
-      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      if (relu) bn_apply_kernel<T, false, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      else bn_apply_kernel<T, false, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
     }
-  });
+  }));
 }
 
 void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
@@ -419,11 +426,12 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
                                                     smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
-  DTG_TPR_SWITCH(g.tpr, bn_apply2_kernel<T><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa, bits));
+  DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH(bn_apply2_kernel<T, RU><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa,
+                                                                                 bits)));
 }
 
 // ---- bwd, projection blocks: dx = a*dp + bx*x + c0 and dx2 = a2*dp + bx2*x2 + c02, one read of dp -----
-template <int TPR>
+template <int TPR, int RU = 4>
 __global__ void __launch_bounds__(kBlk) bn_bwd_dx2_kernel(const bf16_t* __restrict__ dp, const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ x2,
                                                           const float* __restrict__ coef,
@@ -442,12 +450,8 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx2_kernel(const bf16_t* __restri
   load8_f32(coef2 + 2 * C + c0, cc2);
   const long long m0 = (long long)blockIdx.x * rpc;
   const long long m1 = m0 + rpc < M ? m0 + rpc : M;
-  for (long long m = m0 + ty; m < m1; m += RPP) {
-    const long long o = m * C + c0;
-    float g[8], xv[8], x2v[8], o1[8], o2[8];
-    load8_bf16(dp + o, g);
-    load8_bf16(x + o, xv);
-    load8_bf16(x2 + o, x2v);
+  auto finish = [&](const float (&g)[8], const float (&xv)[8], const float (&x2v)[8], long long o) {
+    float o1[8], o2[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       o1[k] = fmaf(a[k], g[k], fmaf(bx[k], xv[k], cc[k]));
@@ -455,6 +459,27 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx2_kernel(const bf16_t* __restri
     }
     store8_bf16(dx + o, o1);
     store8_bf16(dx2 + o, o2);
+  };
+  long long m = m0 + ty;
+  for (; m + (RU - 1) * RPP < m1; m += RU * RPP) {
+    float g[RU][8], xv[RU][8], x2v[RU][8];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const long long o = (m + u * RPP) * C + c0;
+      load8_bf16(dp + o, g[u]);
+      load8_bf16(x + o, xv[u]);
+      load8_bf16(x2 + o, x2v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) finish(g[u], xv[u], x2v[u], (m + u * RPP) * C + c0);
+  }
+  for (; m < m1; m += RPP) {
+    const long long o = m * C + c0;
+    float g[8], xv[8], x2v[8];
+    load8_bf16(dp + o, g);
+    load8_bf16(x + o, xv);
+    load8_bf16(x2 + o, x2v);
+    finish(g, xv, x2v, o);
   }
 }
 
@@ -472,7 +497,8 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
                                                     dbeta2, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
-  DTG_TPR_SWITCH(g.tpr, bn_bwd_dx2_kernel<T><<<ga, kBlk, 0, st>>>(dp, x, x2, ws, ws + 3LL * C, dx, dx2, M, C, rpa));
+  DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH(bn_bwd_dx2_kernel<T, RU><<<ga, kBlk, 0, st>>>(dp, x, x2, ws, ws + 3LL * C, dx,
+                                                                                   dx2, M, C, rpa)));
 }
 
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
@@ -485,13 +511,14 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
                                                     0.f, ws, dgamma, dbeta, 1);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
-  DTG_TPR_SWITCH(g.tpr, {
+  DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
     if (!bn_nt_loads()) {  // DTG_BN_NT=0: plain loads (A/B)
-      if (dres) bn_bwd_dx_kernel<T, false, true, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-      else bn_bwd_dx_kernel<T, false, false, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-    } else if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-    else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-  });
+      if (dres) bn_bwd_dx_kernel<T, false, true, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+      else bn_bwd_dx_kernel<T, false, false, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+    } else if (dres) bn_bwd_dx_kernel<T, false, true, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C,
+                                                                                      rpa);
+    else bn_bwd_dx_kernel<T, false, false, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+  }));
 }
 
 }  // namespace dtg
