@@ -324,10 +324,34 @@ static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long 
   else launch_bn<CF, MODE, true, false>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
+// DTG_BN_GEMM_CFG forces the BN-epilogue GEMM tile (A/B runs): 1 128x128, 2 64x256, 3 128x128 register-
+// pipelined, 4 256x64, 5 128x256 8 waves, 6 256x128 8 waves; 0 = the heuristic below
+static const int g_bn_gemm_cfg = getenv("DTG_BN_GEMM_CFG") ? atoi(getenv("DTG_BN_GEMM_CFG")) : 0;
+
 template <int MODE>
 static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                              const Epi& e, const BnEpi& bn, hipStream_t st) {
-  // same tile choice as gemm_bf16's heuristic
+  switch (g_bn_gemm_cfg) {
+    case 1: return launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    case 2: return launch_bn_cfg<Cfg<64, 256, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    case 3: return launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    case 4: return launch_bn_cfg<Cfg<256, 64, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    case 5: return launch_bn_cfg<Cfg<128, 256, 1, 8>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    case 6: return launch_bn_cfg<Cfg<256, 128, 1, 8>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    default: break;
+  }
+  // measured per ResNet-50 shape (tools/bn_gemm_ab.py, profiles/r03_bn_gemm_tiles): the forward 1x1 expand
+  // GEMMs (K <= 128, N >= 256) on 128x128 tiles (-5..7 % vs 64x256); the backward epilogues (modes 2-4) on the
+  // register-pipelined 128x128 tile from K >= 256 (-4..9 %), except the 64-channel outputs (256x64 stays)
+  if (MODE == 1 && K <= 128 && N >= 256 && M >= 128) {
+    launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    return;
+  }
+  if (MODE >= 2 && MODE <= 4 && K >= 256 && N >= 128) {
+    launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
+    return;
+  }
+  // otherwise the same tile choice as gemm_bf16's heuristic
   if (use_rp(M, N, K)) launch_bn_cfg<Cfg<128, 128, 1, 4, 64, true>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if ((long long)((M + 127) / 128) * ((N + 127) / 128) < 512 && K >= 2048)
     launch_bn_cfg<Cfg<128, 128, 2>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
