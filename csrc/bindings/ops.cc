@@ -489,7 +489,8 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
                                    c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled,
                                    c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
                                    c10::optional<Tensor> invstd2, c10::optional<Tensor> part2,
-                                   c10::optional<std::tuple<int64_t, int64_t>> sub2_hw) {
+                                   c10::optional<std::tuple<int64_t, int64_t>> sub2_hw,
+                                   c10::optional<Tensor> xcoef) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
@@ -558,9 +559,70 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   } else {
     bn.part = part.data_ptr<float>();
     bn.mode = 1;
+    if (xcoef.has_value() && xcoef->defined()) {  // A is the previous BN's input: its apply + relu in the prologue
+      CHECK_IN(*xcoef);
+      CHECK_DT(*xcoef, at::kFloat);
+      TORCH_CHECK(xcoef->numel() == 2LL * K, "xcoef must hold scale[K] and shift[K]");
+      TORCH_CHECK(((uintptr_t)xcoef->data_ptr() % 16) == 0 && K % 8 == 0, "xcoef must be 16-byte aligned");
+      bn.xcoef = xcoef->data_ptr<float>();
+      bn.xc_n = K;
+    }
   }
   dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(o), N, M, N, K, bt, bn, cur_stream());
   return {o, part};
+}
+
+// BN statistics from epilogue partials without the apply pass -> (mean, invstd, coef = [scale[C], shift[C]]);
+// the consumer GEMM applies relu(x * scale + shift) to its operand (gemm_bn xcoef / gemm_xb)
+std::tuple<Tensor, Tensor, Tensor> bn_finalize(Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
+                                               int64_t M, double momentum, double eps) {
+  CHECK_IN(part);
+  CHECK_DT(part, at::kFloat);
+  const int C = (int)gamma.numel();
+  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(part.device());
+  auto fopt = part.options();
+  auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt), coef = at::empty({2LL * C}, fopt);
+  dtg::bn_finalize_part(part.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                        rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(),
+                        sinv.data_ptr<float>(), coef.data_ptr<float>(), M, C, (float)momentum, (float)eps,
+                        cur_stream());
+  return {smean, sinv, coef};
+}
+
+// out[M,N] (+)= A^T relu(B * coef[n] + coef[N + n]) for A [K,M], B [K,N] (both MN-contiguous): the weight
+// gradient of a 1x1 conv whose input is a BN + ReLU output, read from the BN's raw input B
+void gemm_xb(Tensor A, Tensor B, Tensor out, Tensor coef, double beta, int64_t split_k) {
+  CHECK_IN(A);
+  CHECK_IN(B);
+  CHECK_IN(out);
+  CHECK_IN(coef);
+  CHECK_DT(A, at::kBFloat16);
+  CHECK_DT(B, at::kBFloat16);
+  CHECK_DT(coef, at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && out.dim() == 2 && A.size(0) == B.size(0), "A [K,M], B [K,N]");
+  const int K = (int)A.size(0), M = (int)A.size(1), N = (int)B.size(1);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "out must be a contiguous [M, N]");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out fp32/bf16");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "16-byte rows");
+  TORCH_CHECK(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0, "16-byte alignment");
+  TORCH_CHECK(coef.numel() == 2LL * N, "coef must hold scale[N] and shift[N]");
+  c10::DeviceGuard dg(A.device());
+  int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K, 0);
+  Tensor ws;
+  float* wsp = nullptr;
+  if (sk > 1) {
+    ws = at::empty({dtg::gemm_workspace_floats(M, N, K, sk)}, A.options().dtype(at::kFloat));
+    wsp = ws.data_ptr<float>();
+  }
+  dtg::gemm_bf16_xb(cbfp(A), A.stride(0), cbfp(B), B.stride(0), out.data_ptr(), out.stride(0),
+                    out.scalar_type() == at::kBFloat16, M, N, K, (float)beta, coef.data_ptr<float>(), sk, wsp,
+                    cur_stream());
 }
 
 std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad, bool pooled) {
@@ -813,7 +875,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false,
         pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none(),
         pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none(),
-        pybind11::arg("sub2_hw") = pybind11::none());
+        pybind11::arg("sub2_hw") = pybind11::none(), pybind11::arg("xcoef") = pybind11::none());
+  m.def("bn_finalize", &bn_finalize, pybind11::arg("part"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("M"), pybind11::arg("momentum"),
+        pybind11::arg("eps"));
+  m.def("gemm_xb", &gemm_xb, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("out"), pybind11::arg("coef"),
+        pybind11::arg("beta") = 0.0, pybind11::arg("split_k") = 0);
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
         pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
   m.def("bn_bwd2_part", &bn_bwd2_part);

@@ -56,6 +56,11 @@ struct BnEpi {
   // (magic m, shift l of H*W and of W, host-computed: bn_sub2_rows).
   int old_sub2 = 0;
   uint32_t old_hw = 1, old_w = 1, hw_m = 0, hw_l = 0, w_m = 0, w_l = 0;
+  // optional operand prologue: a BatchNorm apply + ReLU, relu(v * xcoef[c] + xcoef[xc_n + c]), applied to the
+  // fragments of the operand that holds the previous BN's raw input (channel c), so the BN output is never
+  // written to memory (gemm_bf16_bn mode 1: the A operand, c = k; gemm_bf16_xb: the B operand, c = column)
+  const float* xcoef = nullptr;
+  int xc_n = 0;
 };
 
 // host: fill the old_sub2 fields of a BnEpi for an H x W image
@@ -79,6 +84,11 @@ long long bn_workspace_floats(long long M, int C);
 void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                       float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
                       int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits = nullptr);
+// statistics from epilogue partials -> smean / sinv, running stats, coef = (scale[C], shift[C]); no apply pass
+// (the consumer GEMM applies relu(x * scale + shift) to its operand fragments: BnEpi::xcoef)
+void bn_finalize_part(const float* part, const float* gamma, const float* beta, float* rmean, float* rvar,
+                      float* smean, float* sinv, float* coef, long long M, int C, float momentum, float eps,
+                      hipStream_t st);
 // y = relu(bn(x) + bn2(r)) with both BNs' statistics from epilogue partials (ws: 4C floats)
 void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* part, const float* part2,
                        const float* gamma, const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
@@ -131,6 +141,11 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 // (bn.mode 1: B is [N,K] (forward); bn.mode 2/3: B is [K,N] (dgrad)).  A is [M,K] K-contiguous.
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st);
+// C (+)= A^T op(B) for MN-contiguous A [K,M] and B [K,N] (a weight gradient, split-K over K) where B is the
+// raw input of a BatchNorm + ReLU: the GEMM reads relu(B * coef[n] + coef[N + n]) (coef from
+// bn_finalize_part) instead of the materialised BN output
+void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, void* C, long long ldc, int c_bf16,
+                  int M, int N, int K, float beta, const float* coef, int split_k, float* ws, hipStream_t st);
 
 // C = act(A * B + bias) (B [K,N], the dgrad layout; aux as in gemm_bf16) and colsum[n] += sum_m C[m, n]
 // in the same epilogue (fp32 atomics; the bias gradient of the layer C is the output gradient of)

@@ -355,6 +355,14 @@ void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float
   bn_apply_launch(g, x, res, y, ws, M, C, relu, st, bits);
 }
 
+// Finalize only: the BN output is produced by its consumer GEMM's operand prologue (BnEpi::xcoef)
+void bn_finalize_part(const float* part, const float* gamma, const float* beta, float* rmean, float* rvar,
+                      float* smean, float* sinv, float* coef, long long M, int C, float momentum, float eps,
+                      hipStream_t st) {
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
+                                                    sinv, momentum, eps, coef, nullptr, nullptr, 1);
+}
+
 // Inference: coefficients from running statistics (tiny launch) then the same apply pass.
 __global__ void bn_infer_coef_kernel(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                                      float eps, int C, float* coef) {

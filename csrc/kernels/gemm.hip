@@ -292,7 +292,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 }
 
 // ---- BN-statistics epilogue (gemm_bf16_bn) ---------------------------------------------------------
-template <class CF, int MODE, bool GUARD, bool PF>
+template <class CF, int MODE, bool GUARD, bool PF, int XF = 0>
 static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                       const Epi& e, const BnEpi& bn, hipStream_t st) {
   using SA = DenseKC<GUARD>;
@@ -300,7 +300,7 @@ static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long
   SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF>), dim3(tiles_m * tiles_n, 1, 1),
+  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
                      dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
 }
 
@@ -360,14 +360,69 @@ static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, lo
   else launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
+// mode 1 with the previous BN applied to A in the operand prologue (BnEpi::xcoef, mfma_gemm.cuh XfA): the
+// single-stage tiles only (the prologue's coefficient loads must not wait behind an in-flight LDS-DMA), with
+// gemm_bn_dispatch's tile choice otherwise
+template <class CF>
+static void launch_bn_xa(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                         const Epi& e, const BnEpi& bn, hipStream_t st) {
+  if ((M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0)) launch_bn<CF, 1, false, false, 1>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else launch_bn<CF, 1, true, false, 1>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
+static void gemm_bn_xa_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                                const Epi& e, const BnEpi& bn, hipStream_t st) {
+  if (skinny(N)) launch_bn_xa<Cfg<256, 64, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (N >= 256 && K > 128 && K <= 256 && M >= 64) launch_bn_xa<Cfg<64, 256, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else launch_bn_xa<Cfg<128, 128, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   Epi e{C, ldc, 1, 1.f, bn.mode == 3 ? beta : 0.f, nullptr, 0};
-  if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
+  if (bn.mode == 1 && bn.xcoef) gemm_bn_xa_dispatch(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.x2) gemm_bn_dispatch<4>(A, lda, B, ldb, M, N, K, e, bn, st);
   else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);
+}
+
+// ---- weight gradient with the B operand's BN + ReLU in the prologue (gemm_bf16_xb) -------------------
+template <class CF, bool GUARD>
+static void launch_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
+                      int kps, const Epi& e, const BnEpi& bn, float* ws, hipStream_t st) {
+  using S = DenseMC<GUARD>;
+  S sa{A, lda, M, K};
+  S sb{B, ldb, N, K};
+  const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
+  hipLaunchKernelGGL((gemm_kernel<CF, false, false, S, S, 0, false, false, 2>), dim3(tiles_m * tiles_n, split_k, 1),
+                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k, kps, e, ws, GemmBatch(), bn);
+  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
+}
+
+template <class CF>
+static void launch_xb_cfg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
+                          int split_k, int kps, const Epi& e, const BnEpi& bn, float* ws, hipStream_t st) {
+  if ((M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0)) launch_xb<CF, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
+  else launch_xb<CF, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
+}
+
+void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, void* C, long long ldc, int c_bf16,
+                  int M, int N, int K, float beta, const float* coef, int split_k, float* ws, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  if (split_k < 1) split_k = 1;
+  int kps = (K + split_k - 1) / split_k;
+  kps = (kps + BK - 1) / BK * BK;
+  if (kps < BK) kps = BK;
+  split_k = (K + kps - 1) / kps;
+  Epi e{C, ldc, c_bf16, 1.f, beta, nullptr, 0};
+  BnEpi bn;
+  bn.xcoef = coef;
+  bn.xc_n = N;
+  // the weight-gradient tile of gemm_bf16 (single-stage 128x128, register-pipelined unless DTG_GEMM_RP=0)
+  if (gemm_rp()) launch_xb_cfg<Cfg<128, 128, 1, 4, 64, true>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
+  else launch_xb_cfg<Cfg<128, 128, 1>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
 }
 
 void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,

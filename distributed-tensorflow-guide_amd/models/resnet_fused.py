@@ -61,6 +61,12 @@ _LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction 
 # linked stride-2 projection: its dgrad writes only the even (h, w) rows, which the next mode-3 GEMM alone
 # reads (no zero-fill of a [N, H, W, C] gradient per stage transition); 0 restores the zero-filled form
 _SUB2 = os.environ.get("DTG_DGRAD_SUB2", "1") != "0"
+# DTG_BN2_FUSE=1: BN2 (+ relu) applied in conv3's operand prologues instead of a separate apply pass (needs
+# _FUSE): the forward GEMM reads y2 and the BN2 coefficients (gemm_bn xcoef), the weight gradient likewise
+# (gemm_xb); a2 and BN2's relu-mask bits are never written.  Off by default: measured slower, ResNet-50 b512
+# 14.46k vs 14.80k img/s -- the prologue costs the forward GEMMs +0.39 ms and the weight gradients +1.2 ms
+# per step against the 0.55 ms apply pass it removes (profiles/r03_bn2_prologue).
+_BN2X = os.environ.get("DTG_BN2_FUSE", "0") == "1"
 
 
 class _Bn3Link:
@@ -100,14 +106,18 @@ _CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "512"))
 _wsplit_cache = {}
 
 
-def _wgrad(dy, x, out):
-    """out (+)= dy^T x for [P, M] dy and [P, N] x (P pixels): a 1x1 conv weight gradient."""
+def _wgrad(dy, x, out, xcoef=None):
+    """out (+)= dy^T x for [P, M] dy and [P, N] x (P pixels): a 1x1 conv weight gradient.  With xcoef the
+    conv's input is relu(x * scale + shift) (a BN apply the forward never materialised, bn_finalize)."""
     tgt = _WSPLIT_WGS if overlap.enabled() else 0
     key = (dy.shape[1], x.shape[1], dy.shape[0], tgt)
     sk = _wsplit_cache.get(key)
     if sk is None:
         sk = _wsplit_cache[key] = lib().gemm_pick_split(key[0], key[1], key[2], False, tgt) if tgt > 0 else 0
-    gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
+    if xcoef is not None:
+        lib().gemm_xb(dy, x, out, xcoef, 1.0, sk)
+    else:
+        gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
 
 
 def _conv_wgrad(dy4, x4, dw, st, pad):
@@ -138,11 +148,21 @@ class _BottleneckFn(torch.autograd.Function):
                                        b1.momentum, b1.eps, True, bits=bits1)
             y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1, pooled=True)
             y2 = y2.view(-1, width)
-            bits2 = _relu_bits(y2)
-            a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
-                                       b2.momentum, b2.eps, True, bits=bits2)
+            if _BN2X:
+                # BN2 + relu applied in conv3's operand prologue (forward GEMM and weight gradient): a2 is never
+                # written; the backward recomputes BN2's relu mask from y2 (mode 2)
+                m2, i2, coef2 = L.bn_finalize(p2, b2.weight, b2.bias, b2.running_mean, b2.running_var, y2.shape[0],
+                                              b2.momentum, b2.eps)
+                a2 = bits2 = None
+                y3, p3 = L.gemm_bn(y2, _mat(w3), 1, pooled=True, xcoef=coef2)
+            else:
+                bits2 = _relu_bits(y2)
+                a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
+                                           b2.momentum, b2.eps, True, bits=bits2)
+                coef2 = None
+                y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
             ctx.bits12 = (bits1, bits2)
-            y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
+            ctx.coef2 = coef2
         else:
             y1 = gemm(x2, True, _mat(w1), True)
             a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
@@ -151,6 +171,7 @@ class _BottleneckFn(torch.autograd.Function):
             a2, m2, i2 = L.bn_fwd_train(y2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.momentum,
                                         b2.eps, True)
             y3 = gemm(a2, True, _mat(w3), True)
+            ctx.coef2 = None
         yd = md = idd = None
         if blk.down is not None:
             bd, wd = blk.down.bn, blk.down.conv.weight
@@ -239,8 +260,14 @@ class _BottleneckFn(torch.autograd.Function):
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
-        with overlap.wgrad_scope(dy3, a2):
-            _wgrad(dy3, a2, g[id(w3)].view(cout, width))
+        coef2 = ctx.coef2
+        ctx.coef2 = None
+        if coef2 is not None:  # conv3's input is relu(bn2(y2)), applied in the weight-gradient GEMM's prologue
+            with overlap.wgrad_scope(dy3, y2, coef2):
+                _wgrad(dy3, y2, g[id(w3)].view(cout, width), coef2)
+        else:
+            with overlap.wgrad_scope(dy3, a2):
+                _wgrad(dy3, a2, g[id(w3)].view(cout, width))
         # BN2 + conv2 (3x3)
         if _FUSE:
             dy2 = L.bn_bwd_part(dp2, y2, q2, b2.weight, m2, i2, False, g[id(b2.weight)], g[id(b2.bias)])[0]

@@ -32,13 +32,15 @@ def test_resnet_tiny_loss_decreases():
 
 @pytest.mark.parametrize("cin,width,stride", [(64, 64, 1), (256, 64, 1), (256, 128, 2), (512, 128, 1)])
 @pytest.mark.parametrize("flat", [False, True])
-@pytest.mark.parametrize("bn_fuse", [True, False])
-def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, monkeypatch):
+@pytest.mark.parametrize("bn_fuse,bn2x", [(True, True), (True, False), (False, False)])
+def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, bn2x, monkeypatch):
     """The hand-written bottleneck backward (with and without BN statistics fused into the conv
-    epilogues) equals the layer-by-layer autograd path."""
+    epilogues, with and without BN2 applied in conv3's operand prologues) equals the layer-by-layer
+    autograd path."""
     from dtg.models.resnet import Bottleneck
     from dtg.models import resnet_fused
     monkeypatch.setattr(resnet_fused, "_FUSE", bn_fuse)
+    monkeypatch.setattr(resnet_fused, "_BN2X", bn2x)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     blocks = []
