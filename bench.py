@@ -5,7 +5,7 @@ images/sec for the whole job, one process per MI355X (RCCL over xGMI).
     python bench.py --gpus N --steps K --warmup W            (N=1 runs in-process)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
 
-Weak scaling: every GPU trains a fixed per-GPU batch (default 512 images of 224x224, synthetic
+Weak scaling: every GPU trains a fixed per-GPU batch (default 1024 images of 224x224, synthetic
 data, random-init weights).  ``--model bert`` measures BASELINE.json config 5 instead (BERT-base
 pre-training, MLM + NSP, seq 128, per-GPU batch 256, fused Adam; sequences/sec).
 
@@ -14,7 +14,10 @@ the per-launch and per-tile fixed costs of every kernel, and it halves the gradi
 all-reduced per image (one model's gradients per step, whatever the batch).  Measured on one MI355X
 (profiles/r02_batch):
 
-- ResNet-50: 10.5k img/s at 128, 12.1k at 256, 12.9k at 384, 13.4k at 512.
+- ResNet-50: 10.5k img/s at 128, 12.1k at 256, 12.9k at 384, 13.4k at 512 (round 2);
+  14.56k at 512, 14.87k at 768, 15.05k at 1024 (round 3, one box, profiles/r03_bn2_prologue).  1024 per GPU
+  (74 GB peak) is the default: at 8 GPUs that is the global batch of 8192 of large-minibatch SGD
+  (linear learning-rate scaling with warmup, Goyal et al. 2017).
 - BERT-base: 6.2k seq/s at 64, 7.6k at 128, 8.2k at 256.
 
 ``--mode async_ps --gpus N`` measures BASELINE.json config 4 (1 PS + N-1 ResNet-50 workers, RCCL
@@ -40,7 +43,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default 512 resnet / 256 bert)")
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch (default 1024 resnet / 256 bert)")
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--image", type=int, default=224)
     # all-reduce bucket size: ResNet-50's 51 MB of bf16 gradients in 8 MB buckets (backward order) leaves
@@ -161,7 +164,7 @@ def main(argv=None):
         metric, unit = "sequences/sec (whole node) BERT-base pre-training sync DP", "sequences/sec"
         conf = {"model": "BERT-base (MLM+NSP)", "seq_len": a.seq, "optimizer": "adam-wd (fused)"}
     else:
-        a.batch = a.batch or 512
+        a.batch = a.batch or 1024
         model = resnet.resnet50().to(device)
         model = model.to(memory_format=torch.channels_last)
         flat = FlatParams(model, compute_dtype=dtype)
