@@ -161,68 +161,119 @@ __global__ void __launch_bounds__(1024) row_sum_kernel(const float* __restrict__
 }
 
 // Word-embedding gradient, sort-free.  Workgroup w owns vocabulary rows [w*VT, (w+1)*VT).  It walks the ids in
-// chunks of 256 (one per thread), compacts the matching token indices IN TOKEN ORDER into an LDS list (wave
-// ballots + a prefix over the 4 waves), and whenever the list fills (or at the end) adds the listed rows of ds
-// into an fp32 LDS accumulator [VT][H]: thread t owns 8-column chunks t, t + 256, ... and walks the list in
-// order, so every vocabulary row is summed in token order by exactly one thread per chunk -- deterministic
-// without atomics.  Rows that received anything are added once into the bf16 gradient.
-constexpr int kEmbVT = 32, kEmbList = 512;
+// chunks of 2048 (8 consecutive tokens per thread, the next chunk's ids loaded under the current one), compacts
+// the matching token indices IN TOKEN ORDER into an LDS list (per-thread hit counts, a block-wide exclusive
+// scan), and whenever the list fills (or at the end) adds the listed rows of ds into an fp32 LDS accumulator
+// [VT][H]: thread t owns 8-column chunk t and walks the list in order, 8 rows of loads in flight at a time, so
+// every vocabulary row is summed in token order by exactly one thread per chunk -- deterministic without
+// atomics.  Rows that received anything are added once into the bf16 gradient.  (The first form walked 256
+// ids per step with one dependent load per step and one per listed row: 420 us per BERT-base step.)
+constexpr int kEmbVT = 32, kEmbList = 2048, kEmbTPT = 8, kEmbChunk = 256 * kEmbTPT;
+
+__device__ __forceinline__ void unpack8_bf16_u4(const uint4& v, float (&o)[8]) {
+  o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+  o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  o[4] = __uint_as_float(v.z << 16); o[5] = __uint_as_float(v.z & 0xffff0000u);
+  o[6] = __uint_as_float(v.w << 16); o[7] = __uint_as_float(v.w & 0xffff0000u);
+}
 
 __global__ void __launch_bounds__(256) emb_word_bwd_owned_kernel(const bf16_t* __restrict__ ds,
                                                                 const long long* __restrict__ ids,
                                                                 bf16_t* __restrict__ gW, int T, int H, int V) {
-  extern __shared__ float acc[];                       // [kEmbVT][H]
+  extern __shared__ float acc[];  // [kEmbVT][H]
   __shared__ int list[kEmbList];
-  __shared__ int wcount[4];
-  __shared__ int nlist_s;
+  __shared__ int wsum[4];
   __shared__ int touched[kEmbVT];
+  typedef __attribute__((address_space(3))) float lds_f;
+  lds_f* accl = (lds_f*)acc;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int v0 = blockIdx.x * kEmbVT;
   const int nch = H >> 3;
-  for (int i = tid; i < kEmbVT * H; i += 256) acc[i] = 0.f;
+  for (int i = tid; i < kEmbVT * H; i += 256) accl[i] = 0.f;
   if (tid < kEmbVT) touched[tid] = 0;
-  if (tid == 0) nlist_s = 0;
   __syncthreads();
-  auto flush = [&](int n) {
+  auto flush = [&](int n) {  // list[0, n) into acc, in list (= token) order per column chunk
     for (int c = tid; c < nch; c += 256) {
-      for (int j = 0; j < n; ++j) {
+      int j = 0;
+      for (; j + 8 <= n; j += 8) {
+        uint4 x[8];
+        int r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int t = list[j + u];
+          r[u] = (int)(ids[t] - v0);
+          x[u] = *reinterpret_cast<const uint4*>(ds + (long long)t * H + c * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          float f[8];
+          unpack8_bf16_u4(x[u], f);
+          lds_f* a = accl + r[u] * H + c * 8;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) a[k] += f[k];
+        }
+      }
+      for (; j < n; ++j) {
         const int t = list[j];
         const int r = (int)(ids[t] - v0);
-        float x[8];
-        load8_bf16(ds + (long long)t * H + c * 8, x);
-        float* a = acc + r * H + c * 8;
+        float f[8];
+        load8_bf16(ds + (long long)t * H + c * 8, f);
+        lds_f* a = accl + r * H + c * 8;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] += x[k];
+        for (int k = 0; k < 8; ++k) a[k] += f[k];
       }
     }
   };
-  for (int base = 0; base < T; base += 256) {
-    const int t = base + tid;
-    const long long id = t < T ? ids[t] : -1;
-    const bool hit = id >= v0 && id < v0 + kEmbVT && id < V;
-    const unsigned long long m = __ballot(hit);
-    if (lane == 0) wcount[wave] = __popcll(m);
-    __syncthreads();
-    int off = nlist_s;
-    for (int w = 0; w < wave; ++w) off += wcount[w];
-    const int total = wcount[0] + wcount[1] + wcount[2] + wcount[3];
-    if (nlist_s + total > kEmbList) {  // flush the list first (every thread sees the same condition)
-      const int n = nlist_s;
-      flush(n);
-      __syncthreads();
-      off -= n;
-      if (tid == 0) nlist_s = 0;
+  long long nid[kEmbTPT];
+  auto load_ids = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < kEmbTPT; ++j) {
+      const int t = base + tid * kEmbTPT + j;
+      nid[j] = t < T ? ids[t] : -1;
     }
-    if (hit) {
-      const int rank = __popcll(m & ((1ull << lane) - 1ull));
-      list[off + rank] = t;
-      touched[(int)(id - v0)] = 1;
+  };
+  int nlist = 0;  // block-uniform
+  load_ids(0);
+  for (int base = 0; base < T; base += kEmbChunk) {
+    long long id[kEmbTPT];
+#pragma unroll
+    for (int j = 0; j < kEmbTPT; ++j) id[j] = nid[j];
+    if (base + kEmbChunk < T) load_ids(base + kEmbChunk);  // next chunk's ids in flight under this one
+    unsigned hm = 0;
+#pragma unroll
+    for (int j = 0; j < kEmbTPT; ++j)
+      if (id[j] >= v0 && id[j] < v0 + kEmbVT && id[j] < V) hm |= 1u << j;
+    // block exclusive scan of the per-thread hit counts (thread order = token order)
+    const int cnt = __popc(hm);
+    int inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
     }
+    if (lane == 63) wsum[wave] = inc;
     __syncthreads();
-    if (tid == 0) nlist_s += total;
-    __syncthreads();
+    int off = inc - cnt;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (total > 0) {
+      if (nlist + total > kEmbList) {  // block-uniform: flush the list first
+        flush(nlist);
+        __syncthreads();
+        nlist = 0;
+      }
+      int k = nlist + off;
+#pragma unroll
+      for (int j = 0; j < kEmbTPT; ++j)
+        if (hm & (1u << j)) {
+          list[k++] = base + tid * kEmbTPT + j;
+          touched[(int)(id[j] - v0)] = 1;
+        }
+      nlist += total;
+    }
+    __syncthreads();  // list written; wsum free for the next chunk
   }
-  flush(nlist_s);
+  flush(nlist);
   __syncthreads();
   for (int r = 0; r < kEmbVT && v0 + r < V; ++r) {
     if (!touched[r]) continue;
@@ -231,7 +282,7 @@ __global__ void __launch_bounds__(256) emb_word_bwd_owned_kernel(const bf16_t* _
       bf16_t* g = gW + (long long)(v0 + r) * H + c * 8;
       load8_bf16(g, o);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] += acc[r * H + c * 8 + k];
+      for (int k = 0; k < 8; ++k) o[k] += accl[r * H + c * 8 + k];
       store8_bf16(g, o);
     }
   }

@@ -332,7 +332,7 @@ def test_emb_word_bwd_owned_matches_index_add():
     equals an fp32 index_add, with a heavily repeated id (more matches than the kernel's list holds, so it
     flushes mid-scan), ids at both vocabulary ends, and existing gradient contents accumulated."""
     torch.manual_seed(3)
-    T_, H, V = 6000, 768, 30528
+    T_, H, V = 12001, 768, 30528  # ids[::3] = 7: 4001 matches, more than the 2048-entry list
     ids = torch.randint(0, V, (T_,), device=dev)
     ids[::3] = 7
     ids[5] = 0
