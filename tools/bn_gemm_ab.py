@@ -4,6 +4,7 @@ DTG_BN_GEMM_CFG (csrc/kernels/gemm.hip gemm_bn_dispatch; 0 = heuristic).  One JS
 us per call and the rate over the compulsory HBM bytes.
 
     for c in 0 1 2 3 4 5 6; do DTG_BN_GEMM_CFG=$c python tools/bn_gemm_ab.py; done
+    DTG_BN_AB_BATCH=1024 ... (the same shapes at per-GPU batch 1024)
 """
 import json
 import os
@@ -43,7 +44,9 @@ def main():
     dev = torch.device("cuda")
     bf = torch.bfloat16
     cfg = os.environ.get("DTG_BN_GEMM_CFG", "0")
+    scale = int(os.environ.get("DTG_BN_AB_BATCH", "512")) // 512  # CASES are ResNet-50 b512 shapes
     for mode, M, N, K in CASES:
+        M *= scale
         A = torch.randn(M, K, device=dev, dtype=bf)
         ch = [torch.rand(N, device=dev) + 0.5 for _ in range(4)]
         if mode == 1:
