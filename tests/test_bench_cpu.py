@@ -56,3 +56,20 @@ def test_async_ps_mode_reports_whole_node_rate():
     assert j["n_gpus"] == 3 and j["config"]["parallelism"] == "ps1+w2" and j["value"] > 0
     assert j["per_worker"] == {"1": 4, "2": 4} and j["lost_workers"] == []
     assert 1 <= j["updates_timed"] <= 8
+
+
+def test_driver_launch_form_eight_ranks_resnet():
+    """The round-end scaling run's exact launch form (torch.distributed.run, 8 ranks on 127.0.0.1, bench.py
+    --gpus 8) with the headline model, shrunk to 32x32 images and batch 2 per rank on gloo: one JSON line
+    from rank 0 with the whole-job rate, dp8 and the global batch."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--image", "32",
+           "--batch", "2", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=_env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    j = _json_line(r.stdout)
+    assert j["n_gpus"] == 8 and j["config"]["parallelism"] == "dp8" and j["config"]["global_batch"] == 16, j
+    assert j["config"]["model"] == "ResNet-50" and j["scaling"] == "weak" and j["value"] > 0
