@@ -25,7 +25,9 @@ point-to-point; see ``_async_ps``).  ``--model mnist`` measures BASELINE.json co
 so it replays as one hipGraph by default).  ``--batch`` overrides the default.  A timed step is the full training step: forward, fused softmax-xent,
 backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD apply.  W untimed
 warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
-is the MAX over ranks; rank 0 prints one JSON line.
+is the MAX over ranks; rank 0 prints one JSON line.  With N > 1 the line also carries ``allreduce_probe``:
+the all-reduce of the whole gradient and of one bucket timed alone AFTER the timed steps (bus bandwidth
+of this job's xGMI links; the scaling curve's communication side).
 """
 import argparse
 import json
@@ -217,6 +219,7 @@ def main(argv=None):
               file=sys.stderr, flush=True)
     gb = a.batch * world
     ips = gb * a.steps / dt
+    probe = _allreduce_probe(dp, a.bucket_mb, world, device, sync) if world > 1 else None
     if rank == 0:
         config = {"model": conf["model"], "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": conf["seq_len"]}
         config.update({k: v for k, v in conf.items() if k not in config})
@@ -227,8 +230,39 @@ def main(argv=None):
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init weights)", "config": config,
-            "final_loss": final_loss}), flush=True)
+            "final_loss": final_loss, **({"allreduce_probe": probe} if probe else {})}), flush=True)
     comm.shutdown()
+
+
+def _allreduce_probe(dp, bucket_mb, world, device, sync):
+    """After the timed steps (outside them): the collective alone, on this job's links -- one all-reduce of
+    the whole gradient (its bytes and dtype) and one of a single bucket, each the median of 5 after 2
+    warm-ups, as algorithm time and bus bandwidth (algbw x 2(N-1)/N, the ring-equivalent per-link rate;
+    SURVEY §7.5 item 7: report busbw next to images/sec, since 2-, 4- and 8-GPU subsets of the xGMI mesh
+    have 1, 3 and 7 links per GPU)."""
+    import torch
+    import torch.distributed as dist
+    from dtg.parallel import comm
+    grads = [g.grad for g in dp.flat]
+    nbytes = sum(t.numel() * t.element_size() for t in grads)
+    dt_ = grads[0].dtype
+    out = {"grad_bytes": nbytes, "dtype": str(dt_).replace("torch.", "")}
+    for name, n in (("full", nbytes), ("bucket", min(nbytes, int(bucket_mb * (1 << 20))))):
+        buf = torch.zeros(max(1, n // grads[0].element_size()), dtype=dt_, device=device)
+        times = []
+        for i in range(7):
+            sync()
+            comm.barrier()
+            t0 = time.perf_counter()
+            dist.all_reduce(buf)
+            sync()
+            if i >= 2:
+                times.append(time.perf_counter() - t0)
+        t = comm.all_reduce_max(sorted(times)[len(times) // 2], device)
+        out[f"{name}_ms"] = round(t * 1e3, 3)
+        out[f"{name}_busbw_GBps"] = round(n / t / 1e9 * 2 * (world - 1) / world, 1)
+        del buf
+    return out
 
 
 def _async_ps(a, rank, world, device):
