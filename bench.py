@@ -27,7 +27,9 @@ backward with bucketed RCCL all-reduce overlapped, and the fused momentum-SGD ap
 warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the job time
 is the MAX over ranks; rank 0 prints one JSON line.  With N > 1 the line also carries ``allreduce_probe``:
 the all-reduce of the whole gradient and of one bucket timed alone AFTER the timed steps (bus bandwidth
-of this job's xGMI links; the scaling curve's communication side).
+of this job's xGMI links), and the same training step re-timed with the collectives switched off
+(``compute_only_ms_per_step``; ``exposed_comm_ms_per_step`` = ms_per_step minus it) -- the scaling curve's
+communication side, measured in the driver's own multi-GPU runs.
 """
 import argparse
 import json
@@ -219,7 +221,28 @@ def main(argv=None):
               file=sys.stderr, flush=True)
     gb = a.batch * world
     ips = gb * a.steps / dt
-    probe = _allreduce_probe(dp, a.bucket_mb, world, device, sync) if world > 1 else None
+    probe = None
+    if world > 1:
+        probe = _allreduce_probe(dp, a.bucket_mb, world, device, sync)
+    if world > 1 and not use_graph:
+        # the same step with the collectives switched off, timed like the real one (after it, outside it):
+        # ms_per_step - compute_only_ms = communication the overlap did not hide
+        n_co = min(a.steps, 10)
+        dp.set_comm(False)
+        step()
+        sync()
+        comm.barrier()
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(n_co):
+            step()
+        sync()
+        comm.barrier()
+        sync()
+        co = comm.all_reduce_max(time.perf_counter() - t1, device) / n_co
+        dp.set_comm(True)
+        probe["compute_only_ms_per_step"] = round(co * 1e3, 3)
+        probe["exposed_comm_ms_per_step"] = round(dt / a.steps * 1e3 - co * 1e3, 3)
     if rank == 0:
         config = {"model": conf["model"], "global_batch": gb, "per_gpu_batch": a.batch, "seq_len": conf["seq_len"]}
         config.update({k: v for k, v in conf.items() if k not in config})

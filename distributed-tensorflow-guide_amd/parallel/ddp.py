@@ -53,6 +53,7 @@ class DataParallel:
         forced = os.environ.get("DTG_DDP_FORCE") == "1" and dist.is_available() and dist.is_initialized()
         self.overlap = overlap and (self.world > 1 or forced)
         self._force = forced
+        self._comm = True  # set_comm(False): gradients stay rank-local (bench.py's compute-only timing)
         self._cstreams = {}
         self.buckets = []
         self._hooks = []
@@ -135,7 +136,7 @@ class DataParallel:
         self._done.add(p)
         b = self._param_bucket[p]
         b.pending -= 1
-        if b.pending == 0:
+        if b.pending == 0 and self._comm:
             self._launch(b)
 
     # -- step ------------------------------------------------------------------------------------
@@ -147,6 +148,9 @@ class DataParallel:
     def finish(self):
         """Wait for every bucket's all-reduce (launching any that did not fire)."""
         overlap.join()  # (normally already joined at the end of backward)
+        if not self._comm:
+            self._reset()
+            return
         if self.world == 1 and not self._force:
             return
         for b in self.buckets:
@@ -154,6 +158,13 @@ class DataParallel:
                 self._launch(b)
         for b in self.buckets:
             b.work.wait()
+        self._reset()
+
+    def set_comm(self, on):
+        """Turn the gradient collectives off (on=False: every rank steps on its own gradients) or back on.
+        bench.py times a few steps this way after the timed region, so its JSON line can split a multi-GPU
+        step into compute and exposed communication."""
+        self._comm = bool(on)
         self._reset()
 
     def broadcast_parameters(self, src=0):

@@ -75,3 +75,4 @@ def test_driver_launch_form_eight_ranks_resnet():
     assert j["config"]["model"] == "ResNet-50" and j["scaling"] == "weak" and j["value"] > 0
     p = j["allreduce_probe"]  # the collective alone, after the timed steps: bytes of the whole gradient
     assert p["grad_bytes"] > 25_000_000 * 2 * 0.9 and p["full_busbw_GBps"] > 0 and p["bucket_ms"] > 0, p
+    assert p["compute_only_ms_per_step"] > 0 and "exposed_comm_ms_per_step" in p, p
