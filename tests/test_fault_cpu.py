@@ -85,7 +85,9 @@ def test_ssgd_backup_workers_survive_a_dead_worker():
     its 3rd run.  The chief keeps aggregating the two live workers' gradients to the last step, and the PS
     counts the dead worker as finished (its watched connection dropped) so it exits too."""
     from _cluster import last_int_after, run_cluster
-    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 3, ["--init_tokens", "0"],
+    # the guide's pacing at 1/10 (the chief 0.2 s per step): with none, the two live workers could finish all
+    # 10 steps before worker 2 reached its 3rd run, and it then exited cleanly instead of dying
+    out = run_cluster("Synchronous-SGD/ssgd.py", 1, 3, ["--init_tokens", "0", "--observe_sleep", "0.1"],
                       env={"DTG_FAULT": "kill_worker_at_run:2@3"}, timeout=120)
     assert out[("worker", 2)][0] == 23
     for t in (0, 1):
