@@ -572,6 +572,19 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   return {o, part};
 }
 
+// experimental: direct 3x3 conv (C = K = 64, stride 1, pad 1) from an LDS halo tile (csrc/kernels/conv_halo.hip)
+Tensor conv_halo_fwd(Tensor x, Tensor w) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C, "w must be [64, 3, 3, C]");
+  TORCH_CHECK(dtg::conv3x3_halo_supported(C, (int)w.size(0), H, W), "conv_halo_fwd: C = K = 64, H % 4 == 0, W <= 64");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, H, W, 64}, x.options());
+  dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream());
+  return y;
+}
+
 // BN statistics from epilogue partials without the apply pass -> (mean, invstd, coef = [scale[C], shift[C]]);
 // the consumer GEMM applies relu(x * scale + shift) to its operand (gemm_bn xcoef / gemm_xb)
 std::tuple<Tensor, Tensor, Tensor> bn_finalize(Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
@@ -879,6 +892,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_finalize", &bn_finalize, pybind11::arg("part"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("M"), pybind11::arg("momentum"),
         pybind11::arg("eps"));
+  m.def("conv_halo_fwd", &conv_halo_fwd, pybind11::arg("x"), pybind11::arg("w"));
   m.def("gemm_xb", &gemm_xb, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("out"), pybind11::arg("coef"),
         pybind11::arg("beta") = 0.0, pybind11::arg("split_k") = 0);
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },

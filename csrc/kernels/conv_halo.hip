@@ -1,0 +1,134 @@
+// Experimental (round 3): 3x3 / stride 1 / pad 1 convolution for 64 input and 64 output channels (ResNet-50's
+// layer-1 conv2, NHWC bf16) as a DIRECT convolution from an LDS halo tile, to test whether the implicit-GEMM
+// kernel's L2 traffic is what limits it (profiles/r03_conv_l2: the implicit GEMM gathers every input pixel once
+// per filter tap, 9x through L2, with the L2 channels busy 94 % of every cycle).
+//
+// One workgroup (4 waves) = one band of TH = 4 output rows of one image (4 x W pixels, W <= 60) x all 64 output
+// channels.  The band's input rows with their 1-pixel halo, (TH + 2) x (W + 2) pixels x 64 channels, are staged
+// ONCE into LDS (zeros outside the image), together with all 9 taps of the weights; every tap's A fragments are
+// then read from the halo at the shifted pixel, so each input byte crosses L2 about (TH + 2) / TH times instead
+// of 9.  Layout of both LDS images: [pixel or output channel][64 channels] with the 16-byte chunk XOR-swizzled
+// by (row & 7), as frag_kc reads it.  Output through an LDS staging pass as 16-byte stores.
+#include "dtg/common.h"
+#include "dtg/kernels.h"
+#include "dtg/mfma_gemm.cuh"
+
+namespace dtg {
+using namespace gemm;
+
+namespace {
+
+constexpr int kTH = 4, kC = 64;
+
+__device__ __forceinline__ int swz_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__global__ void __launch_bounds__(256) conv3x3_halo_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ y, int N, int H, int W) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int HW2 = W + 2;
+  const int halo_px = (kTH + 2) * HW2;
+  lds_char* halo = smem;                      // [halo_px][64]
+  lds_char* wt = smem + halo_px * 128;        // [9][64 k][64 c]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bands = H / kTH;
+  const int n = blockIdx.x / bands, oh0 = (blockIdx.x % bands) * kTH;
+
+  // ---- stage the halo (zero outside the image) and the weights: 16-byte chunks, plain loads + LDS stores
+  for (int i = tid; i < halo_px * 8; i += 256) {
+    const int hp = i >> 3, ch = i & 7;
+    const int hr = hp / HW2, hc = hp - hr * HW2;
+    const int ih = oh0 - 1 + hr, iw = hc - 1;
+    u32x4v v = {0u, 0u, 0u, 0u};
+    if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+      v = *reinterpret_cast<const u32x4v*>(x + (((long long)n * H + ih) * W + iw) * kC + ch * 8);
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(halo + swz_off(hp, ch)) = v;
+  }
+  for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t = r*3 + s][k][c]
+    const int ch = i & 7, k = (i >> 3) & 63, t = i >> 9;
+    const u32x4v v = *reinterpret_cast<const u32x4v*>(w + ((long long)k * 9 + t) * kC + ch * 8);
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(wt + t * 64 * 128 + swz_off(k, ch)) = v;
+  }
+  __syncthreads();
+
+  // ---- wave `wave` owns output pixels [64 wave, 64 wave + 64) of the band (the band has kTH * W <= 240)
+  const int npx = kTH * W;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int hbase[4];  // halo pixel of this lane's output pixel in each 16-row fragment, tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int p = wave * 64 + i * 16 + (lane & 15);
+    p = p < npx ? p : npx - 1;  // rows past the band compute a duplicate; not stored
+    const int oh = p / W, ow = p - oh * W;
+    hbase[i] = oh * HW2 + ow;
+  }
+  const int g = lane >> 4;
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const int dr = t / 3, ds = t - dr * 3, dpx = dr * HW2 + ds;
+    const lds_char* wtt = wt + t * 64 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      v8bf a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const lds_v8bf*>(halo + swz_off(hbase[i] + dpx, ks * 4 + g));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *reinterpret_cast<const lds_v8bf*>(wtt + swz_off(j * 16 + (lane & 15), ks * 4 + g));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // halo / weights no longer read: reuse the LDS for the output staging
+
+  // ---- epilogue: each wave stages its 64 x 64 tile as bf16 [pixel][64] (128-B rows) and stores 16-B chunks
+  lds_char* st = smem + wave * 64 * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pr = i * 16 + g * 4 + r, col = j * 16 + (lane & 15);
+        *reinterpret_cast<__attribute__((address_space(3))) bf16_t*>(st + pr * 128 + col * 2) = f2bf(acc[i][j][r]);
+      }
+  __syncthreads();
+  const long long out0 = ((long long)n * H + oh0) * W;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int idx = k * 64 + lane, pr = idx >> 3, ch = idx & 7;
+    const int p = wave * 64 + pr;
+    if (p < npx) {
+      const u32x4v v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4v*>(st + pr * 128 + ch * 16);
+      *reinterpret_cast<u32x4v*>(y + (out0 + p) * kC + ch * 8) = v;
+    }
+  }
+}
+
+}  // namespace
+
+size_t conv3x3_halo_lds(int W) { return (size_t)(kTH + 2) * (W + 2) * 128 + 9 * 64 * 128; }
+
+int conv3x3_halo_supported(int C, int K, int H, int W) {
+  return C == kC && K == kC && H % kTH == 0 && W >= 1 && kTH * W <= 256 && conv3x3_halo_lds(W) <= 160 * 1024;
+}
+
+void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv3x3_halo_kernel, dim3(N * (H / kTH)), dim3(256), conv3x3_halo_lds(W), st, x, w, y, N, H, W);
+  DTG_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dtg

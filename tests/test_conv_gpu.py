@@ -121,3 +121,17 @@ def test_stem_pack_pairs_matches_pad(N, C, H, W, pad, S):
     got, wgot, _ = stem_pairs(x.to(DEV), w.to(DEV), 2, pad)
     assert got.shape == ref.shape and torch.equal(got.cpu(), ref)
     assert torch.equal(wgot.cpu(), wref)
+
+
+def test_conv_halo_fwd_matches_fp32_reference():
+    """Experimental direct 3x3 conv from an LDS halo tile (csrc/kernels/conv_halo.hip; not used by the models,
+    profiles/r03_conv_l2): equals the fp32 convolution, image edges in every band."""
+    import torch.nn.functional as F
+    from dtg.ops._native import lib
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    x = torch.randn(3, 56, 56, 64, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(dev, torch.bfloat16)
+    y = lib().conv_halo_fwd(x, w)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
