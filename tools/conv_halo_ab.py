@@ -50,6 +50,11 @@ def main():
     N = a.batch
     x = torch.randn(N, 56, 56, 64, device=dev, dtype=torch.bfloat16)
     fl = 2.0 * N * 56 * 56 * 64 * 64 * 9
+    # at full size (more bands than CUs: the persistent form walks several per workgroup) against the GEMM
+    yh, yg = L.conv_halo_fwd(x, w).float(), L.conv_fwd(x, w, 1, 1).float()
+    rel3 = ((yh - yg).norm() / yg.norm()).item()
+    print(f"batch {N}: halo vs implicit GEMM rel diff {rel3:.2e}", flush=True)
+    assert rel3 < 1e-2, rel3
     for r in range(2):
         th = timeit(lambda: L.conv_halo_fwd(x, w))
         tg = timeit(lambda: L.conv_fwd(x, w, 1, 1))
