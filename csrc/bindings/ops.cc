@@ -585,6 +585,20 @@ Tensor conv_halo_fwd(Tensor x, Tensor w) {
   return y;
 }
 
+// the same with the BatchNorm forward statistics of the output: (y, part) as conv_fwd_bn returns them
+std::tuple<Tensor, Tensor> conv_halo_fwd_bn(Tensor x, Tensor w) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C, "w must be [64, 3, 3, C]");
+  TORCH_CHECK(dtg::conv3x3_halo_supported(C, 64, H, W, 1), "conv_halo_fwd_bn: C = K = 64, H % 4 == 0, W <= 56");
+  c10::DeviceGuard dg(x.device());
+  auto y = at::empty({N, H, W, 64}, x.options());
+  auto part = bn_part(x, 64, false);
+  dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream(), part.data_ptr<float>());
+  return {y, part};
+}
+
 // BN statistics from epilogue partials without the apply pass -> (mean, invstd, coef = [scale[C], shift[C]]);
 // the consumer GEMM applies relu(x * scale + shift) to its operand (gemm_bn xcoef / gemm_xb)
 std::tuple<Tensor, Tensor, Tensor> bn_finalize(Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
@@ -651,6 +665,15 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
   auto part = bn_part(x, K, pooled);
+  // DTG_CONV_HALO=1: 3x3 / s1 / p1, 64 -> 64 (ResNet-50 layer 1) through the direct halo-tile conv
+  // (conv_halo.hip): 16 % faster alone (338 vs 400 us at batch 1024 with the statistics), but it holds all of
+  // every CU's LDS while it runs, and the whole training step measured no faster (profiles/r03_conv_l2), so the
+  // implicit GEMM stays the default
+  static const bool halo_on = getenv("DTG_CONV_HALO") && getenv("DTG_CONV_HALO")[0] == '1';
+  if (halo_on && R == 3 && S == 3 && stride == 1 && pad == 1 && dtg::conv3x3_halo_supported(C, K, H, W, 1)) {
+    dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream(), part.data_ptr<float>());
+    return {y, part};
+  }
   dtg::BnEpi bn;
   bn.part = part.data_ptr<float>();
   bn.mode = 1;
@@ -898,6 +921,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
         pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
   m.def("bn_bwd2_part", &bn_bwd2_part);
+  m.def("conv_halo_fwd_bn", &conv_halo_fwd_bn, pybind11::arg("x"), pybind11::arg("w"));
   m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("pooled") = false);
   m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),

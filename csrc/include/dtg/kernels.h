@@ -144,11 +144,13 @@ void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
 // C (+)= A^T op(B) for MN-contiguous A [K,M] and B [K,N] (a weight gradient, split-K over K) where B is the
 // raw input of a BatchNorm + ReLU: the GEMM reads relu(B * coef[n] + coef[N + n]) (coef from
 // bn_finalize_part) instead of the materialised BN output
-// Experimental direct 3x3 / stride 1 / pad 1 conv for C = K = 64 from an LDS halo tile (conv_halo.hip)
-int conv3x3_halo_supported(int C, int K, int H, int W);
-void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st);
 void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, void* C, long long ldc, int c_bf16,
                   int M, int N, int K, float beta, const float* coef, int split_k, float* ws, hipStream_t st);
+// Direct 3x3 / stride 1 / pad 1 conv for C = K = 64 from an LDS halo tile (conv_halo.hip); with part, also the
+// BatchNorm forward statistics of the output (BnEpi mode 1 partials, kBnStatSlots x 2 x 64)
+int conv3x3_halo_supported(int C, int K, int H, int W, int stats = 0);
+void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st,
+                      float* part = nullptr);
 
 // C = act(A * B + bias) (B [K,N], the dgrad layout; aux as in gemm_bf16) and colsum[n] += sum_m C[m, n]
 // in the same epilogue (fp32 atomics; the bias gradient of the layer C is the output gradient of)

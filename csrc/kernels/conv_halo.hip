@@ -163,8 +163,13 @@ __global__ void __launch_bounds__(256) conv3x3_halo_kernel(const bf16_t* __restr
 // after its run of bands (uniform loop bound).
 constexpr int kPF = 11;  // 16-byte halo chunks per thread: (kTH + 2) * (W + 2) * 8 <= 256 * kPF
 
+// part != nullptr: BatchNorm forward statistics of the stored (bf16) output, sum and sum of squares per
+// channel, kept in registers across the workgroup's bands and added once into part[blockIdx % kBnStatSlots]
+// (the conv_fwd_bn contract, kernels.h: BnEpi mode 1)
+template <bool STATS>
 __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                             bf16_t* __restrict__ y, int N, int H, int W) {
+                                                             bf16_t* __restrict__ y, int N, int H, int W,
+                                                             float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
   const int HW2 = W + 2, halo_px = (kTH + 2) * HW2, hbytes = halo_px * 128;
@@ -216,6 +221,7 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     const int oh = p / W, ow = p - oh * W;
     hbase[i] = oh * HW2 + ow;
   }
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};  // channel j*16 + lane%16
   int cur = 0;
   for (int band = b0; band < b1; ++band) {
     if (band + 1 < b1) gload(band + 1);
@@ -254,7 +260,13 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int pr = i * 16 + g * 4 + r, col = j * 16 + (lane & 15);
-          *reinterpret_cast<__attribute__((address_space(3))) bf16_t*>(st + pr * 128 + col * 2) = f2bf(acc[i][j][r]);
+          const bf16_t v = f2bf(acc[i][j][r]);
+          *reinterpret_cast<__attribute__((address_space(3))) bf16_t*>(st + pr * 128 + col * 2) = v;
+          if constexpr (STATS) {  // rows past the band (duplicates) weigh 0
+            const float f = wave * 64 + pr < npx ? bf2f(v) : 0.f;
+            ssum[j] += f;
+            ssq[j] += f * f;
+          }
         }
     __syncthreads();
     const int n = band / bands, oh0 = (band - n * bands) * kTH;
@@ -271,6 +283,24 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     if (band + 1 < b1) lstore(hbuf[cur ^ 1]);
     __syncthreads();  // next halo visible; this band's staging reads done
     cur ^= 1;
+  }
+  if constexpr (STATS) {  // lanes l, l + 16, l + 32, l + 48 hold the same channels: fold, then one atomic per channel and wave
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        ssum[j] += __shfl_xor(ssum[j], o);
+        ssq[j] += __shfl_xor(ssq[j], o);
+      }
+    }
+    if (g == 0 && b0 < b1) {
+      float* slot = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * kC;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(slot + j * 16 + lane, ssum[j]);
+        atomicAdd(slot + kC + j * 16 + lane, ssq[j]);
+      }
+    }
   }
 }
 
@@ -290,26 +320,30 @@ static size_t conv3x3_halo_lds(int W, int mode) {
   return a > stage ? a : stage;
 }
 
-int conv3x3_halo_supported(int C, int K, int H, int W) {
-  const int mode = halo_mode();
+int conv3x3_halo_supported(int C, int K, int H, int W, int stats) {
+  const int mode = stats ? 0 : halo_mode();
   if (mode == 0 && (kTH + 2) * (W + 2) * 8 > 256 * kPF) return 0;
   return C == kC && K == kC && H % kTH == 0 && W >= 1 && kTH * W <= 256 && conv3x3_halo_lds(W, mode) <= 160 * 1024;
 }
 
-void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st) {
+void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st, float* part) {
   static int n_cu = 0;
   if (!n_cu) {
     for (const void* f : {(const void*)conv3x3_halo_kernel<false>, (const void*)conv3x3_halo_kernel<true>,
-                          (const void*)conv3x3_halo_pp_kernel})
+                          (const void*)conv3x3_halo_pp_kernel<false>,
+                          (const void*)conv3x3_halo_pp_kernel<true>})
       DTG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int dev = 0;
     DTG_HIP_CHECK(hipGetDevice(&dev));
     DTG_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  const int mode = halo_mode(), total = N * (H / kTH);
+  const int mode = part ? 0 : halo_mode(), total = N * (H / kTH);
   const size_t lds = conv3x3_halo_lds(W, mode);
-  if (mode == 0)
-    hipLaunchKernelGGL(conv3x3_halo_pp_kernel, dim3(total < n_cu ? total : n_cu), dim3(256), lds, st, x, w, y, N, H, W);
+  const dim3 grid(total < n_cu ? total : n_cu);
+  if (part)
+    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<true>, grid, dim3(256), lds, st, x, w, y, N, H, W, part);
+  else if (mode == 0)
+    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<false>, grid, dim3(256), lds, st, x, w, y, N, H, W, part);
   else if (mode == 1)
     hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(total), dim3(256), lds, st, x, w, y, N, H, W);
   else

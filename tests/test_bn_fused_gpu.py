@@ -83,7 +83,8 @@ def _pack_mask(x, mean, inv, gamma, beta):
     return (m << torch.arange(8, device=x.device, dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
 
 
-@pytest.mark.parametrize("C,K,H,R,st,pad", [(64, 64, 14, 3, 1, 1), (128, 128, 14, 3, 2, 1), (64, 256, 8, 1, 1, 0),
+@pytest.mark.parametrize("C,K,H,R,st,pad", [(64, 64, 14, 3, 1, 1), (64, 64, 16, 3, 1, 1), (128, 128, 14, 3, 2, 1),
+                                            (64, 256, 8, 1, 1, 0),
                                             (256, 512, 7, 3, 1, 1)])
 def test_conv_bn_fwd_and_dgrad_stats(C, K, H, R, st, pad):
     dev = torch.device("cuda")

@@ -59,8 +59,9 @@ def main():
         th = timeit(lambda: L.conv_halo_fwd(x, w))
         tg = timeit(lambda: L.conv_fwd(x, w, 1, 1))
         tb = timeit(lambda: L.conv_fwd_bn(x, w, 1, 1))
+        ths = timeit(lambda: L.conv_halo_fwd_bn(x, w))
         print(f"round {r}: halo {th:.1f} us ({fl / th / 1e6:.0f} TF/s)  implicit GEMM {tg:.1f} us  "
-              f"implicit GEMM + BN stats {tb:.1f} us", flush=True)
+              f"| with BN stats: halo {ths:.1f} us  conv_fwd_bn {tb:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
