@@ -124,7 +124,9 @@ def main(argv=None):
             return loss
         return step
 
-    rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo")
+    # async PS survives a lost worker on its own: no fail-stop rank watchdog there
+    rank, local, world, device = comm.init("nccl" if torch.cuda.is_available() else "gloo",
+                                           watchdog=a.mode != "async_ps")
     if world != a.gpus:
         # a mislabelled point on the scaling curve is worse than no point
         comm.shutdown()
@@ -224,7 +226,9 @@ def main(argv=None):
     probe = None
     if world > 1:
         probe = _allreduce_probe(dp, a.bucket_mb, world, device, sync)
-    if world > 1 and not use_graph:
+    emu = dp.emulate  # DTG_COMM_EMULATE (parallel/ddp.py): one-card stand-in for an N-rank all-reduce
+    if (world > 1 or emu) and not use_graph:
+        probe = probe or ({"comm_emulate": emu} if emu else {})
         # the same step with the collectives switched off, timed like the real one (after it, outside it):
         # ms_per_step - compute_only_ms = communication the overlap did not hide
         n_co = min(a.steps, 10)

@@ -945,6 +945,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adagrad_apply", &adagrad_apply);
   m.def("adam_apply", &adam_apply);
   m.def("axpby", &axpby);
+  m.def("comm_spin", [](double seconds, int64_t wgs, int64_t lds_bytes) {
+    dtg::comm_spin(seconds, (int)wgs, (int)lds_bytes, cur_stream());
+  }, pybind11::arg("seconds"), pybind11::arg("wgs") = 32, pybind11::arg("lds_bytes") = 0);
+  m.def("launch_probe", [](int64_t grid, int64_t lds_bytes) {
+    dtg::launch_probe((int)grid, (int)lds_bytes, cur_stream());
+  });
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_infer", &bn_fwd_infer);

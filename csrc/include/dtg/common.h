@@ -4,6 +4,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+
+#include <stdexcept>
 
 namespace dtg {
 
@@ -105,10 +108,27 @@ inline int grid_for(long long n_vec, int block, int cap = 2048) {
 
 }  // namespace dtg
 
-#define DTG_HIP_CHECK(expr)                                                              \
-  do {                                                                                   \
-    hipError_t _e = (expr);                                                              \
-    if (_e != hipSuccess) {                                                              \
-      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
-    }                                                                                    \
+namespace dtg {
+// A failed HIP call or kernel launch (too much LDS for a new shape, an invalid grid, a dead device) raises:
+// pybind11 turns std::runtime_error into a Python RuntimeError, so no op returns an unwritten output.
+[[noreturn]] inline void hip_fail(hipError_t e, const char* what, const char* file, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "dtg: %s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+  throw std::runtime_error(buf);
+}
+
+// After every <<<>>> launch.  hipErrorNotReady is the "still running" answer of an earlier stream / event
+// query (the caching allocator polls events), never a launch failure.
+inline void launch_check(const char* file, int line) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess && e != hipErrorNotReady) hip_fail(e, "kernel launch", file, line);
+}
+}  // namespace dtg
+
+#define DTG_HIP_CHECK(expr)                                         \
+  do {                                                              \
+    hipError_t _e = (expr);                                         \
+    if (_e != hipSuccess) ::dtg::hip_fail(_e, #expr, __FILE__, __LINE__); \
   } while (0)
+
+#define DTG_LAUNCH_CHECK() ::dtg::launch_check(__FILE__, __LINE__)

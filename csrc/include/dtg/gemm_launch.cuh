@@ -110,13 +110,13 @@ inline void launch(const bf16_t* A, long long lda, const bf16_t* B, long long ld
   if constexpr (AK) {  // (K-contiguous A = forward / dgrad GEMMs; weight gradients go through split-K)
     if (split_k == 1 && fast_epi(e, N) && (bt.count == 1 || ((bt.sc_b | bt.sc_h) & 7) == 0)) {
       hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB, 0, true>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K,
-                         tiles_n, split_k, kps, e, ws, bt, BnEpi());
+                         tiles_n, split_k, kps, e, ws, bt, BnEpi()); DTG_LAUNCH_CHECK();
       if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
       return;
     }
   }
   hipLaunchKernelGGL((gemm_kernel<CF, AK, BK_, SA, SB>), grid, dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                       kps, e, ws, bt, BnEpi());
+                       kps, e, ws, bt, BnEpi()); DTG_LAUNCH_CHECK();
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 

@@ -23,6 +23,10 @@ void adam_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* m, f
 void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st);
 void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
 
+// ---- emulated blocking collective (comm_emu.hip; parallel/ddp.py DTG_COMM_EMULATE) ------------------
+void comm_spin(double seconds, int wgs, int lds_bytes, hipStream_t st);
+void launch_probe(int grid, int lds_bytes, hipStream_t st);
+
 // ---- BatchNorm statistics fused into a GEMM / implicit-GEMM epilogue (dtg/bn_epi.cuh) ----------
 // mode 1 (forward): per output column c, sum and sum of squares of the stored (bf16) output.
 // mode 2 (backward through BN -> ReLU): the epilogue turns the GEMM result g (= dL/da, a = relu(bn(x)))

@@ -696,7 +696,7 @@ void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   dim3 grid(B * nh, (S + 16 * kFwdWaves - 1) / (16 * kFwdWaves));
   hipLaunchKernelGGL(attn_fwd_kernel<512>, grid, dim3(64 * kFwdWaves), fwd_lds(S), st, qkv, mask, out, lse, S, nh, 0.125f, th,
-                     ds, seed);
+                     ds, seed); DTG_LAUNCH_CHECK();
 }
 
 void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, const float* mask,
@@ -716,15 +716,16 @@ void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const floa
   if (S > 128) {
     const dim3 grid(B * nh, (S + kLongKeys - 1) / kLongKeys);
     hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(512), dkv_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                       0.125f, th, ds, seed);
+                       0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
     hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(512), dq_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                       0.125f, th, ds, seed);
-  } else if (S == 64)
+                       0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+  } else if (S == 64) {
     hipLaunchKernelGGL(attn_bwd_kernel<64>, dim3(B * nh), dim3(512), bwd_lds(64), st, qkv, o, dout, lse, mask, dqkv,
-                       nh, 0.125f, th, ds, seed);
-  else
+                       nh, 0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+  } else {
     hipLaunchKernelGGL(attn_bwd_kernel<128>, dim3(B * nh), dim3(512), bwd_lds(128), st, qkv, o, dout, lse, mask,
-                       dqkv, nh, 0.125f, th, ds, seed);
+                       dqkv, nh, 0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+  }
 }
 
 }  // namespace dtg

@@ -323,11 +323,11 @@ static void bn_apply_launch(const BnGeom& g, const bf16_t* x, const bf16_t* res,
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
-      else bn_apply_kernel<T, true, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      if (relu) { bn_apply_kernel<T, true, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits); DTG_LAUNCH_CHECK(); }
+      else { bn_apply_kernel<T, true, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits); DTG_LAUNCH_CHECK(); }
     } else {
-      if (relu) bn_apply_kernel<T, false, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
-      else bn_apply_kernel<T, false, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits);
+      if (relu) { bn_apply_kernel<T, false, true, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits); DTG_LAUNCH_CHECK(); }
+      else { bn_apply_kernel<T, false, false, RU><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa, bits); DTG_LAUNCH_CHECK(); }
     }
   }));
 }
@@ -339,9 +339,9 @@ void bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
   float* part = ws;
   float* coef = ws + (long long)g.nchunk * 2 * C;
   dim3 grid(g.nchunk, g.gy);
-  DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part));
+  DTG_TPR_SWITCH(g.tpr, bn_stats_kernel<T><<<grid, kBlk, 0, st>>>(x, M, C, g.rows_per_chunk, part)); DTG_LAUNCH_CHECK();
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, 0, gamma, beta, rmean, rvar, smean, sinv,
-                                                    momentum, eps, coef, nullptr, nullptr);
+                                                    momentum, eps, coef, nullptr, nullptr); DTG_LAUNCH_CHECK();
   bn_apply_launch(g, x, res, y, coef, M, C, relu, st);
 }
 
@@ -351,7 +351,7 @@ void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float
                       int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1);
+                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1); DTG_LAUNCH_CHECK();
   bn_apply_launch(g, x, res, y, ws, M, C, relu, st, bits);
 }
 
@@ -360,7 +360,7 @@ void bn_finalize_part(const float* part, const float* gamma, const float* beta, 
                       float* smean, float* sinv, float* coef, long long M, int C, float momentum, float eps,
                       hipStream_t st) {
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                    sinv, momentum, eps, coef, nullptr, nullptr, 1);
+                                                    sinv, momentum, eps, coef, nullptr, nullptr, 1); DTG_LAUNCH_CHECK();
 }
 
 // Inference: coefficients from running statistics (tiny launch) then the same apply pass.
@@ -379,17 +379,17 @@ void bn_fwd_infer(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ga
                   hipStream_t st) {
   const BnGeom g = bn_geom(M, C);
   float* coef = ws;
-  bn_infer_coef_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, rmean, rvar, eps, C, coef);
+  bn_infer_coef_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, rmean, rvar, eps, C, coef); DTG_LAUNCH_CHECK();
   dim3 grid(g.nchunk, g.gy);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (res) {
-      if (relu) bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
-      else bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      if (relu) { bn_apply_kernel<T, true, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa); DTG_LAUNCH_CHECK(); }
+      else { bn_apply_kernel<T, true, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa); DTG_LAUNCH_CHECK(); }
     } else {
-      if (relu) bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
-      else bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa);
+      if (relu) { bn_apply_kernel<T, false, true><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa); DTG_LAUNCH_CHECK(); }
+      else { bn_apply_kernel<T, false, false><<<ga, kBlk, 0, st>>>(x, res, y, coef, M, C, rpa); DTG_LAUNCH_CHECK(); }
     }
   });
 }
@@ -402,21 +402,21 @@ void bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, const float* gam
   float* coef = ws + (long long)g.nchunk * 2 * C;
   dim3 grid(g.nchunk, g.gy);
   DTG_TPR_SWITCH(g.tpr, {
-    if (relu) bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
-    else bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part);
+    if (relu) { bn_bwd_reduce_kernel<T, true><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part); DTG_LAUNCH_CHECK(); }
+    else { bn_bwd_reduce_kernel<T, false><<<grid, kBlk, 0, st>>>(dy, y, x, smean, sinv, M, C, g.rows_per_chunk, part); DTG_LAUNCH_CHECK(); }
   });
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, g.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr, nullptr,
                                                     const_cast<float*>(smean), const_cast<float*>(sinv), 0.f, 0.f,
-                                                    coef, dgamma, dbeta);
+                                                    coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, {
     if (relu) {
-      if (dres) bn_bwd_dx_kernel<T, true, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
-      else bn_bwd_dx_kernel<T, true, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
+      if (dres) { bn_bwd_dx_kernel<T, true, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
+      else { bn_bwd_dx_kernel<T, true, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
     } else {
-      if (dres) bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
-      else bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa);
+      if (dres) { bn_bwd_dx_kernel<T, false, true><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
+      else { bn_bwd_dx_kernel<T, false, false><<<ga, kBlk, 0, st>>>(dy, y, x, coef, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
     }
   });
 }
@@ -429,13 +429,13 @@ void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float*
                        uint8_t* bits) {
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1);
+                                                    sinv, momentum, eps, ws, nullptr, nullptr, 1); DTG_LAUNCH_CHECK();
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, 0, gamma2, beta2, rmean2, rvar2,
-                                                    smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1);
+                                                    smean2, sinv2, momentum, eps, ws + 2LL * C, nullptr, nullptr, 1); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH(bn_apply2_kernel<T, RU><<<ga, kBlk, 0, st>>>(x, r, y, ws, ws + 2LL * C, M, C, rpa,
-                                                                                 bits)));
+                                                                                 bits))); DTG_LAUNCH_CHECK();
 }
 
 // ---- bwd, projection blocks: dx = a*dp + bx*x + c0 and dx2 = a2*dp + bx2*x2 + c02, one read of dp -----
@@ -498,15 +498,15 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
-                                                    0.f, ws, dgamma, dbeta, 1);
+                                                    0.f, ws, dgamma, dbeta, 1); DTG_LAUNCH_CHECK();
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part2, kBnStatSlots, M, C, accum ? 2 : 1, gamma2, nullptr,
                                                     nullptr, nullptr, const_cast<float*>(smean2),
                                                     const_cast<float*>(sinv2), 0.f, 0.f, ws + 3LL * C, dgamma2,
-                                                    dbeta2, 1);
+                                                    dbeta2, 1); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH(bn_bwd_dx2_kernel<T, RU><<<ga, kBlk, 0, st>>>(dp, x, x2, ws, ws + 3LL * C, dx,
-                                                                                   dx2, M, C, rpa)));
+                                                                                   dx2, M, C, rpa))); DTG_LAUNCH_CHECK();
 }
 
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
@@ -516,16 +516,16 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
   const BnGeom g = bn_geom(M, C);
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
-                                                    0.f, ws, dgamma, dbeta, 1);
+                                                    0.f, ws, dgamma, dbeta, 1); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
     if (!bn_nt_loads()) {  // DTG_BN_NT=0: plain loads (A/B)
-      if (dres) bn_bwd_dx_kernel<T, false, true, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-      else bn_bwd_dx_kernel<T, false, false, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
-    } else if (dres) bn_bwd_dx_kernel<T, false, true, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C,
-                                                                                      rpa);
-    else bn_bwd_dx_kernel<T, false, false, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa);
+      if (dres) { bn_bwd_dx_kernel<T, false, true, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
+      else { bn_bwd_dx_kernel<T, false, false, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
+    } else if (dres) { bn_bwd_dx_kernel<T, false, true, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C,
+                                                                                      rpa); DTG_LAUNCH_CHECK(); }
+    else { bn_bwd_dx_kernel<T, false, false, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
   }));
 }
 

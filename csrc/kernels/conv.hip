@@ -476,8 +476,8 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 1) conv_fwd_kernel<CF, 1><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
-    else conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
+    if (bn.mode == 1) { conv_fwd_kernel<CF, 1><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   const int sc = conv_stages(0, M, K, R * S * C);
   if (conv_skinny(K)) run_sched<256, 64>(sc, run);
@@ -493,8 +493,8 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 1) conv_fwd_kernel<CF, 1, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
-    else conv_fwd_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn);
+    if (bn.mode == 1) { conv_fwd_kernel<CF, 1, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_fwd_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   if (conv_skinny(K)) run(Cfg<256, 64, 1>());
   else run(Cfg<128, 128, 1>());
@@ -556,9 +556,9 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
   const int sc = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s));
   auto run = [&](auto cf) {
     using CF = decltype(cf);
-    if (bn.mode == 2) conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
-    else if (bn.mode == 3) conv_dgrad_s_kernel<CF, 3><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
-    else conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn);
+    if (bn.mode == 2) { conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else if (bn.mode == 3) { conv_dgrad_s_kernel<CF, 3><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   if (skinny) run_sched<256, 64>(sc, run);
   else run_sched<128, 128>(dgrad_sched(sc, G), run);
@@ -574,16 +574,16 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 2) conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
-    else if (bn.mode == 3) conv_dgrad_kernel<CF, 3><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
-    else conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn);
+    if (bn.mode == 2) { conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else if (bn.mode == 3) { conv_dgrad_kernel<CF, 3><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   auto run_t = [&](auto cf) {  // K-contiguous transposed weights
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 2) conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
-    else if (bn.mode == 3) conv_dgrad_kernel<CF, 3, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
-    else conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn);
+    if (bn.mode == 2) { conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else if (bn.mode == 3) { conv_dgrad_kernel<CF, 3, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   const int sc = conv_stages(1, M, C, R * S * K);
   if (wT && sc == 1) {
@@ -627,7 +627,7 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
     using CF = decltype(cf);
     const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
     dim3 grid(tm * tn, split);
-    conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps);
+    conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps); DTG_LAUNCH_CHECK();
   };
   const int sc = conv_stages(2);
   if (K <= 64) run_sched<64, 256>(sc, run);  // 64 output channels: one 64-row tile

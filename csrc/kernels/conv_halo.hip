@@ -348,7 +348,7 @@ void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
     hipLaunchKernelGGL(conv3x3_halo_kernel<true>, dim3(total), dim3(256), lds, st, x, w, y, N, H, W);
   else
     hipLaunchKernelGGL(conv3x3_halo_kernel<false>, dim3(total), dim3(256), lds, st, x, w, y, N, H, W);
-  DTG_HIP_CHECK(hipGetLastError());
+  DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

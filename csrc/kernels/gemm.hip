@@ -218,10 +218,10 @@ void gemm_force_cfg(int cfg) { g_forced_cfg = cfg; }
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
   if (N % 8 == 0 && split_k > 16) {
     const long long plane = (long long)M * N;
-    splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e);
+    splitk_reduce_par_kernel<<<(unsigned)((plane + 255) / 256), 256, 0, st>>>(ws, split_k, M, N, e); DTG_LAUNCH_CHECK();
   } else {
     const long long total = (long long)M * ((N + 7) / 8);
-    splitk_reduce_kernel<<<grid_for(total, 256, 1 << 16), 256, 0, st>>>(ws, split_k, M, N, e);
+    splitk_reduce_kernel<<<grid_for(total, 256, 1 << 16), 256, 0, st>>>(ws, split_k, M, N, e); DTG_LAUNCH_CHECK();
   }
 }
 
@@ -301,7 +301,7 @@ static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
-                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
+                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn); DTG_LAUNCH_CHECK();
 }
 
 // DTG_BN_PF: 0 never prefetch, 2 always, default 1 = the shape rule in launch_bn_cfg
@@ -397,7 +397,7 @@ static void launch_xb(const bf16_t* A, long long lda, const bf16_t* B, long long
   S sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
   hipLaunchKernelGGL((gemm_kernel<CF, false, false, S, S, 0, false, false, 2>), dim3(tiles_m * tiles_n, split_k, 1),
-                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k, kps, e, ws, GemmBatch(), bn);
+                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k, kps, e, ws, GemmBatch(), bn); DTG_LAUNCH_CHECK();
   if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
 }
 

@@ -275,7 +275,7 @@ static void launch8(const bf16_t* A, long long lda, const bf16_t* B, long long l
   const int tiles_m = (M + g8::BM - 1) / g8::BM, tiles_n = (N + g8::BN - 1) / g8::BN;
   dim3 grid(tiles_m * tiles_n, split_k);
   hipLaunchKernelGGL((gemm8_kernel<AK, BK_, SA, SB>), grid, dim3(g8::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k,
-                     kps, e, ws);
+                     kps, e, ws); DTG_LAUNCH_CHECK();
 }
 
 template <bool GUARD>

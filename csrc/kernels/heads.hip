@@ -2,7 +2,8 @@
 // no sort, no framework loss or index kernels on the step):
 //
 //   gather_rows        hm[i] = seq[(i / P) * S + pos[i]]          masked-LM rows (pos: [B, P] positions)
-//   scatter_rows_add   dseq[(i / P) * S + pos[i]] += dhm[i]         (pos == null: rows i * S, the [CLS] rows)
+//   scatter_rows_add   dseq[(i / P) * S + pos[i]] += dhm[i]         (pos == null: rows i * S, the [CLS] rows);
+//                      repeated positions within a sequence accumulate (added in order, one wave per sequence)
 //   nsp_loss_fwd       logits = pooled Wn^T + bn ([B, 2]), softmax cross-entropy, mean over B, + the MLM
 //                      loss -> the total pre-training loss (one workgroup: a deterministic reduction order)
 //   nsp_loss_bwd       dlogits = (p - onehot) * g / B;  dpre = (dlogits Wn) * (1 - pooled^2)  (tanh');
@@ -32,18 +33,25 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const bf16_t* __restri
   for (int c = lane; c < (H >> 3); c += 64) d[c] = s[c];
 }
 
+// One wave per (sequence, 512-column block): the wave adds that sequence's P rows IN ORDER, so positions that
+// repeat within a sequence (padded masked_lm_positions are commonly all 0) accumulate every update -- no lost
+// read-modify-write race, and a deterministic summation order.  pos == null: P = 1, row i -> dst row i * S.
 __global__ void __launch_bounds__(256) scatter_rows_add_kernel(bf16_t* __restrict__ dst, const long long* __restrict__ pos,
-                                                               const bf16_t* __restrict__ src, int R, int P, int S, int H) {
+                                                               const bf16_t* __restrict__ src, int nseq, int P, int S,
+                                                               int H) {
   const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= R) return;
-  const long long row = pos ? (long long)(i / P) * S + pos[i] : (long long)i * S;
-  for (int c = lane; c < (H >> 3); c += 64) {
-    float a[8], b[8];
+  const int nvec = H >> 3, wps = (nvec + 63) / 64;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = wv / wps, c = (wv % wps) * 64 + lane;
+  if (b >= nseq || c >= nvec) return;
+  for (int j = 0; j < P; ++j) {
+    const long long i = (long long)b * P + j;
+    const long long row = pos ? (long long)b * S + pos[i] : i * S;
+    float a[8], v[8];
     load8_bf16(dst + row * H + c * 8, a);
-    load8_bf16(src + (long long)i * H + c * 8, b);
+    load8_bf16(src + i * H + c * 8, v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] += b[k];
+    for (int k = 0; k < 8; ++k) a[k] += v[k];
     store8_bf16(dst + row * H + c * 8, a);
   }
 }
@@ -292,29 +300,32 @@ __global__ void __launch_bounds__(256) emb_word_bwd_owned_kernel(const bf16_t* _
 
 void gather_rows(const bf16_t* src, const long long* pos, bf16_t* out, int R, int P, int S, int H, hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((R + 3) / 4), dim3(256), 0, st, src, pos, out, R, P, S, H);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((R + 3) / 4), dim3(256), 0, st, src, pos, out, R, P, S, H); DTG_LAUNCH_CHECK();
 }
 
 void scatter_rows_add(bf16_t* dst, const long long* pos, const bf16_t* src, int R, int P, int S, int H,
                       hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(scatter_rows_add_kernel, dim3((R + 3) / 4), dim3(256), 0, st, dst, pos, src, R, P, S, H);
+  if (!pos) P = 1;
+  const int nseq = R / P, waves = nseq * (((H >> 3) + 63) / 64);
+  hipLaunchKernelGGL(scatter_rows_add_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, dst, pos, src, nseq, P, S, H);
+  DTG_LAUNCH_CHECK();
 }
 
 void nsp_loss_fwd(const bf16_t* pooled, const bf16_t* wn, const float* bn, const long long* labels, const float* extra,
                   float* probs, float* out, int B, int H, hipStream_t st) {
   hipLaunchKernelGGL(nsp_loss_fwd_kernel, dim3(1), dim3(kNspThreads), 0, st, pooled, wn, bn, labels, extra, probs, out,
-                     B, H);
+                     B, H); DTG_LAUNCH_CHECK();
 }
 
 void nsp_loss_bwd(const bf16_t* pooled, const bf16_t* wn, const float* probs, const long long* labels, const float* gout,
                   bf16_t* dpre, bf16_t* gwn, float* gbn, int B, int H, hipStream_t st) {
   hipLaunchKernelGGL(nsp_loss_bwd_kernel, dim3((H + 63) / 64), dim3(1024), 0, st, pooled, wn, probs, labels, gout, dpre,
-                     gwn, gbn, B, H);
+                     gwn, gbn, B, H); DTG_LAUNCH_CHECK();
 }
 
 void row_sum(const float* x, float* out, long long n, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(row_sum_kernel, dim3(1), dim3(1024), 0, st, x, out, n, scale);
+  hipLaunchKernelGGL(row_sum_kernel, dim3(1), dim3(1024), 0, st, x, out, n, scale); DTG_LAUNCH_CHECK();
 }
 
 void emb_word_bwd_owned(const bf16_t* ds, const long long* ids, bf16_t* gW, int T, int H, int V, hipStream_t st) {
@@ -326,8 +337,7 @@ void emb_word_bwd_owned(const bf16_t* ds, const long long* ids, bf16_t* gW, int 
     attr = true;
   }
   hipLaunchKernelGGL(emb_word_bwd_owned_kernel, dim3((V + kEmbVT - 1) / kEmbVT), dim3(256), lds, st, ds, ids, gW, T, H,
-                     V);
-  DTG_HIP_CHECK(hipGetLastError());
+                     V); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -106,8 +106,8 @@ void im2col(const bf16_t* x, bf16_t* cols, int N, int H, int W, int C, int R, in
   ColGeom g = col_geom(N, H, W, C, R, S, stride, pad, Kp);
   const bool vec = (C % 8 == 0) && (Kp % 8 == 0);
   const long long total = (long long)N * g.P * g.Q * (vec ? Kp / 8 : Kp);
-  if (vec) hipLaunchKernelGGL(im2col_kernel<true>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, cols, g);
-  else hipLaunchKernelGGL(im2col_kernel<false>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, cols, g);
+  if (vec) { hipLaunchKernelGGL(im2col_kernel<true>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, cols, g); DTG_LAUNCH_CHECK(); }
+  else { hipLaunchKernelGGL(im2col_kernel<false>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, cols, g); DTG_LAUNCH_CHECK(); }
 }
 
 void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,
@@ -115,8 +115,8 @@ void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, 
   ColGeom g = col_geom(N, H, W, C, R, S, stride, pad, Kp);
   const bool vec = (C % 8 == 0) && (Kp % 8 == 0);
   const long long total = (long long)N * H * W * (vec ? C / 8 : C);
-  if (vec) hipLaunchKernelGGL(col2im_kernel<true>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, dcols, dx, g);
-  else hipLaunchKernelGGL(col2im_kernel<false>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, dcols, dx, g);
+  if (vec) { hipLaunchKernelGGL(col2im_kernel<true>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, dcols, dx, g); DTG_LAUNCH_CHECK(); }
+  else { hipLaunchKernelGGL(col2im_kernel<false>, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, dcols, dx, g); DTG_LAUNCH_CHECK(); }
 }
 
 }  // namespace dtg

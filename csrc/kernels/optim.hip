@@ -136,7 +136,11 @@ static void launch_apply_dev(const OP& op, float* w, bf16_t* mirror, void* grad,
                              hipStream_t st) {
   const int block = 256;
   const int grid = grid_for((n >> 3) + 1, block, 2048);
-#define DTG_L(G, M) apply_kernel_dev<OP, G, M, NST><<<grid, block, 0, st>>>(w, mirror, grad, s0, s1, n, gscale, zero_grad, op, hyper)
+#define DTG_L(G, M)                                                                                              \
+  do {                                                                                                          \
+    apply_kernel_dev<OP, G, M, NST><<<grid, block, 0, st>>>(w, mirror, grad, s0, s1, n, gscale, zero_grad, op, hyper); \
+    DTG_LAUNCH_CHECK();                                                                                          \
+  } while (0)
   if (grad_bf16) { if (mirror) DTG_L(true, true); else DTG_L(true, false); }
   else { if (mirror) DTG_L(false, true); else DTG_L(false, false); }
 #undef DTG_L
@@ -193,8 +197,8 @@ __global__ void __launch_bounds__(256) axpby_kernel(float* __restrict__ acc, con
 
 void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st) {
   const int grid = grid_for((n >> 3) + 1, 256, 2048);
-  if (g_bf16) axpby_kernel<true><<<grid, 256, 0, st>>>(acc, g, n, alpha, beta);
-  else axpby_kernel<false><<<grid, 256, 0, st>>>(acc, g, n, alpha, beta);
+  if (g_bf16) { axpby_kernel<true><<<grid, 256, 0, st>>>(acc, g, n, alpha, beta); DTG_LAUNCH_CHECK(); }
+  else { axpby_kernel<false><<<grid, 256, 0, st>>>(acc, g, n, alpha, beta); DTG_LAUNCH_CHECK(); }
 }
 
 // fp32 -> bf16 mirror refresh (after a PS pull / checkpoint restore)
@@ -212,7 +216,7 @@ __global__ void __launch_bounds__(256) f32_to_bf16_kernel(const float* __restric
 }
 
 void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st) {
-  f32_to_bf16_kernel<<<grid_for((n >> 3) + 1, 256, 2048), 256, 0, st>>>(x, y, n);
+  f32_to_bf16_kernel<<<grid_for((n >> 3) + 1, 256, 2048), 256, 0, st>>>(x, y, n); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -151,23 +151,23 @@ void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, 
                  int Q, hipStream_t st) {
   PoolGeom g{N, H, W, C, P, Q, k, s, pad};
   const long long total = (long long)N * P * Q * (C / 8);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, x, y, idx, g);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, x, y, idx, g); DTG_LAUNCH_CHECK();
 }
 
 void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int k, int s, int pad,
                  int P, int Q, hipStream_t st) {
   PoolGeom g{N, H, W, C, P, Q, k, s, pad};
   const long long total = (long long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, dy, idx, dx, g);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, dy, idx, dx, g); DTG_LAUNCH_CHECK();
 }
 
 void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((C / 8 + 31) / 32, N), dim3(256), 0, st, x, y, N, HW, C);
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((C / 8 + 31) / 32, N), dim3(256), 0, st, x, y, N, HW, C); DTG_LAUNCH_CHECK();
 }
 
 void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
   const long long total = (long long)N * HW * (C / 8);
-  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, dy, dx, N, HW, C);
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, dy, dx, N, HW, C); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

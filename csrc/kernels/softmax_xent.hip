@@ -162,6 +162,7 @@ void softmax_xent(const void* x, int x_bf16, const long long* label, long long B
   else
     softmax_xent_kernel<float, false><<<(unsigned)B, 256, 0, st>>>((const float*)x, label, V, scale, loss, (float*)dx,
                                                                   lse);
+  DTG_LAUNCH_CHECK();
 }
 
 void softmax_xent_bwd(const void* x, int x_bf16, const long long* label, const float* lse, long long B, int V,
@@ -175,6 +176,7 @@ void softmax_xent_bwd(const void* x, int x_bf16, const long long* label, const f
   else
     softmax_xent_bwd_kernel<float, false><<<(unsigned)B, 256, 0, st>>>((const float*)x, label, lse, V, scale, g,
                                                                       (float*)dx);
+  DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -434,7 +434,7 @@ void stem_pack_pairs(const bf16_t* x, bf16_t* xp, int N, int H, int W, int C, in
                      hipStream_t st) {
   const long long total = (long long)N * Hp * (Wp / 2);
   hipLaunchKernelGGL(stem_pack_pairs_kernel, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, x, xp, N, H, W, C,
-                     pad, Hp, Wp / 2);
+                     pad, Hp, Wp / 2); DTG_LAUNCH_CHECK();
 }
 
 static StemGeom stem_geom(int N, int H, int W, int C, int k, int s, int pad, int P, int Q) {
@@ -470,7 +470,7 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                       int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st) {
   const long long M = (long long)N * H * W;
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                         sinv, momentum, eps, coef, nullptr, nullptr, 0);
+                                                         sinv, momentum, eps, coef, nullptr, nullptr, 0); DTG_LAUNCH_CHECK();
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   const long long total = (long long)N * P * Q * (C / 8);
   // 3x3 windows (ResNet): the unrolled form with raw-vector loads (DTG_STEM_POOL_KT=0: the runtime loop)
@@ -479,6 +479,7 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
     hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
   else
     hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+  DTG_LAUNCH_CHECK();
 }
 
 void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
@@ -494,25 +495,24 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
     const unsigned nb = (unsigned)(N * (H / kStemBandRows));
     DTG_HIP_CHECK(hipMemsetAsync(part, 0, (size_t)kBnStatSlots * 2 * C * sizeof(float), st));
     hipLaunchKernelGGL(stem_bwd_band_kernel<false>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
-                       sinv, nullptr, g, part, nullptr);
+                       sinv, nullptr, g, part, nullptr); DTG_LAUNCH_CHECK();
     bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr,
                                                            nullptr, nullptr, const_cast<float*>(smean),
-                                                           const_cast<float*>(sinv), 0.f, 0.f, coef, dgamma, dbeta);
+                                                           const_cast<float*>(sinv), 0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
     hipLaunchKernelGGL(stem_bwd_band_kernel<true>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
-                       sinv, coef, g, nullptr, dy);
-    DTG_HIP_CHECK(hipGetLastError());  // a failed launch must not leave dy / the partials as garbage
+                       sinv, coef, g, nullptr, dy); DTG_LAUNCH_CHECK();
     return;
   }
   dim3 grid(bg.nchunk, bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_reduce_kernel<T><<<grid, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, g, M,
-                                                                         bg.rows_per_chunk, part));
+                                                                         bg.rows_per_chunk, part)); DTG_LAUNCH_CHECK();
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, bg.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                          nullptr, const_cast<float*>(smean), const_cast<float*>(sinv),
-                                                         0.f, 0.f, coef, dgamma, dbeta);
+                                                         0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(bg, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_dx_kernel<T><<<ga, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, coef, g, M,
-                                                                   rpa, dy));
+                                                                   rpa, dy)); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

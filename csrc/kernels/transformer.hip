@@ -514,8 +514,8 @@ void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float*
   const float si = p_in > 0.f ? 1.f / (1.f - p_in) : 1.f, so = p_out > 0.f ? 1.f / (1.f - p_out) : 1.f;
   const int nch = (H / 8 + 63) / 64;
 #define DTG_LNF(NC)                                                                                                   \
-  hipLaunchKernelGGL(ln_fwd_kernel<NC>, dim3(rows_grid(T)), dim3(256), 0, st, h, res, gamma, beta, y, s_out, mean, \
-                     rstd, T, H, eps, ti, si, seed_in, to, so, seed_out)
+  do { hipLaunchKernelGGL(ln_fwd_kernel<NC>, dim3(rows_grid(T)), dim3(256), 0, st, h, res, gamma, beta, y, s_out, mean, \
+                     rstd, T, H, eps, ti, si, seed_in, to, so, seed_out); DTG_LAUNCH_CHECK(); } while (0)
   if (nch <= 1) DTG_LNF(1);
   else if (nch == 2) DTG_LNF(2);
   else DTG_LNF(4);
@@ -549,8 +549,8 @@ void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* 
   const int nc4 = (H / 4 + 63) / 64;  // 4-element chunks per lane (H = 768: 3)
   const size_t lds = (size_t)kRowsPerBlock * 3 * H * sizeof(float);
 #define DTG_LNB(NC)                                                                                                  \
-  hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
-                     ws, dbias, T, H, ti, si, seed_in, to, so, seed_out)
+  do { hipLaunchKernelGGL(ln_bwd_kernel<NC>, dim3(nb), dim3(256), lds, st, dy, s, gamma, mean, rstd, ds_out, dh_out,     \
+                     ws, dbias, T, H, ti, si, seed_in, to, so, seed_out); DTG_LAUNCH_CHECK(); } while (0)
   if (nc4 <= 1) DTG_LNB(1);
   else if (nc4 == 2) DTG_LNB(2);
   else if (nc4 == 3) DTG_LNB(3);
@@ -559,7 +559,7 @@ void ln_bwd(const bf16_t* dy, const bf16_t* s, const float* gamma, const float* 
 #undef DTG_LNB
   const int ncols = dbias ? 3 * H : 2 * H;
   hipLaunchKernelGGL(ln_param_reduce_kernel, dim3((ncols + 63) / 64, 8), dim3(256), 0, st, ws, nb, H, ncols, dgamma,
-                     dbeta, dbias);
+                     dbeta, dbias); DTG_LAUNCH_CHECK();
 }
 
 int attn_max_keys() { return 64 * 16; }
@@ -572,8 +572,8 @@ void attn_softmax_fwd(const float* sc, const float* mask, bf16_t* P, bf16_t* Pd,
   if (!th) Pd = P;
   const int nj = (Sk + 63) / 64;
 #define DTG_SMF(NJ)                                                                                            \
-  hipLaunchKernelGGL(attn_softmax_fwd_kernel<NJ>, dim3(rows_grid(rows)), dim3(256), 0, st, sc, mask, P, Pd, rows, \
-                     rows_per_b, Sk, th, scl, seed)
+  do { hipLaunchKernelGGL(attn_softmax_fwd_kernel<NJ>, dim3(rows_grid(rows)), dim3(256), 0, st, sc, mask, P, Pd, rows, \
+                     rows_per_b, Sk, th, scl, seed); DTG_LAUNCH_CHECK(); } while (0)
   if (nj <= 1) DTG_SMF(1);
   else if (nj == 2) DTG_SMF(2);
   else if (nj <= 4) DTG_SMF(4);
@@ -587,7 +587,7 @@ void attn_softmax_bwd(const bf16_t* P, const bf16_t* Pd, const float* dPd, bf16_
   if (rows <= 0) return;
   const int nj = (Sk + 63) / 64;
 #define DTG_SMB(NJ) \
-  hipLaunchKernelGGL(attn_softmax_bwd_kernel<NJ>, dim3(rows_grid(rows)), dim3(256), 0, st, P, Pd, dPd, dS, rows, Sk, scale)
+  do { hipLaunchKernelGGL(attn_softmax_bwd_kernel<NJ>, dim3(rows_grid(rows)), dim3(256), 0, st, P, Pd, dPd, dS, rows, Sk, scale); DTG_LAUNCH_CHECK(); } while (0)
   if (nj <= 1) DTG_SMB(1);
   else if (nj == 2) DTG_SMB(2);
   else if (nj <= 4) DTG_SMB(4);
@@ -610,24 +610,24 @@ void colsum(const bf16_t* x, long long ld, int T, int N, const long long* sel, i
   if (T <= 0 || N <= 0) return;
   dim3 grid((N + 255) / 256, splits);
   float* aout = (!out_bf16 && accumulate) ? (float*)out : nullptr;
-  if (nsel <= 1) hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout);
-  else hipLaunchKernelGGL(colsum_partial_kernel<2>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout);
+  if (nsel <= 1) { hipLaunchKernelGGL(colsum_partial_kernel<1>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout); DTG_LAUNCH_CHECK(); }
+  else { hipLaunchKernelGGL(colsum_partial_kernel<2>, grid, dim3(256), 0, st, x, ld, T, N, sel, ws, aout); DTG_LAUNCH_CHECK(); }
   if (aout) return;
   const int nsn = (nsel <= 1 ? 1 : 2) * N;
   hipLaunchKernelGGL(colsum_reduce_kernel, dim3((nsn + 255) / 256), dim3(256), 0, st, ws, splits, nsn, out, out_bf16,
-                     accumulate);
+                     accumulate); DTG_LAUNCH_CHECK();
 }
 
 void emb_fwd(const long long* ids, const long long* tt, const bf16_t* word, const bf16_t* pos, const bf16_t* type,
              bf16_t* s, int T, int S, int H, hipStream_t st) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(emb_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, st, ids, tt, word, pos, type, s, T, S, H);
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3(rows_grid(T)), dim3(256), 0, st, ids, tt, word, pos, type, s, T, S, H); DTG_LAUNCH_CHECK();
 }
 
 void emb_word_bwd(const bf16_t* ds, const long long* sorted, const long long* perm, bf16_t* gW, int T, int H,
                   hipStream_t st) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(emb_word_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, st, ds, sorted, perm, gW, T, H);
+  hipLaunchKernelGGL(emb_word_bwd_kernel, dim3(rows_grid(T)), dim3(256), 0, st, ds, sorted, perm, gW, T, H); DTG_LAUNCH_CHECK();
 }
 
 // Position-embedding grad, batch split: one workgroup per position, G groups of threads each summing
@@ -678,10 +678,10 @@ void emb_pos_bwd(const bf16_t* ds, bf16_t* gP, int T, int S, int H, hipStream_t 
   if (H % 8 == 0 && nch <= 128) {
     const int threads = nch * 8;  // G = 8 groups
     hipLaunchKernelGGL(emb_pos_bwd_split_kernel<8>, dim3(S), dim3(threads), (size_t)8 * nch * 8 * sizeof(float), st,
-                       ds, gP, T, S, H);
+                       ds, gP, T, S, H); DTG_LAUNCH_CHECK();
     return;
   }
-  hipLaunchKernelGGL(emb_pos_bwd_kernel, dim3(rows_grid(S)), dim3(256), 0, st, ds, gP, T, S, H);
+  hipLaunchKernelGGL(emb_pos_bwd_kernel, dim3(rows_grid(S)), dim3(256), 0, st, ds, gP, T, S, H); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -132,6 +132,10 @@ class _Control:
 
     def __init__(self, is_ps, rank):
         from .. import _runtime
+        from . import comm
+        # a lost worker is survivable here (serve() continues with the rest): the fail-stop rank watchdog that
+        # comm.init starts for multi-rank jobs would instead end every rank DTG_RANK_TIMEOUT after the loss
+        comm.stop_watchdog()
         _instances[0] += 1
         key = "dtg.aps.ctl.%d" % _instances[0]
         store = dist.distributed_c10d._get_default_store()
@@ -374,8 +378,11 @@ class AsyncPSServer:
         return self
 
     def _sync(self):
+        """Wait for the apply stream only: a device-wide synchronize would also wait on every pair stream,
+        and a parameter send to a worker that was lost mid-run never completes with RCCL (those sends are
+        deliberately left unjoined)."""
         if self.dev.type == "cuda":
-            torch.cuda.synchronize(self.dev)
+            torch.cuda.current_stream(self.dev).synchronize()
 
     def serve(self, poll_sleep=None):
         """Serve requests in arrival order until every worker is done or lost.  (``poll_sleep`` is

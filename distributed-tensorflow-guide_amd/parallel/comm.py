@@ -28,9 +28,11 @@ def env_rank():
         os.environ.get("WORLD_SIZE", "1"))
 
 
-def init(backend=None, timeout_s=None):
+def init(backend=None, timeout_s=None, watchdog=True):
     """Initialise the default process group from the environment (no-op for world_size 1).
 
+    ``watchdog=False`` skips the fail-stop rank :class:`Watchdog` -- for jobs that survive a lost rank on
+    their own (the async parameter server, parallel/async_ps.py, also stops it when it is constructed).
     Returns (rank, local_rank, world, device)."""
     rank, local, world = env_rank()
     # DTG_BACKEND=gloo with DTG_GLOO_DEVICE=cuda rehearses the multi-rank GPU path on ONE card
@@ -67,7 +69,7 @@ def init(backend=None, timeout_s=None):
             timeout_s = float(os.environ.get("DTG_COLLECTIVE_TIMEOUT", "600"))
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-        if world > 1 and os.environ.get("DTG_WATCHDOG", "1") == "1":
+        if world > 1 and watchdog and os.environ.get("DTG_WATCHDOG", "1") == "1":
             Watchdog.start(rank, world)
     return rank, local, world, device
 
@@ -142,6 +144,14 @@ class Watchdog:
             pass
 
 
+def stop_watchdog():
+    """Stop this rank's fail-stop watchdog, if one runs (it also marks the rank finished for the peers'
+    watchdogs, so a job whose ranks all call this never fail-stops on a lost peer)."""
+    if Watchdog._inst is not None:
+        Watchdog._inst.stop()
+        Watchdog._inst = None
+
+
 def barrier():
     if dist.is_initialized():
         if dist.get_backend() == "nccl":
@@ -159,8 +169,6 @@ def all_reduce_max(x: float, device):
 
 
 def shutdown():
-    if Watchdog._inst is not None:
-        Watchdog._inst.stop()
-        Watchdog._inst = None
+    stop_watchdog()
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -29,6 +29,19 @@ from ..utils.trace import trace_range
 _LAUNCH = os.environ.get("DTG_DDP_LAUNCH", "side")  # stream a bucket's collective is enqueued from
 
 
+def _parse_emulate(spec):
+    """DTG_COMM_EMULATE="<busbw GB/s>[,<ranks>[,<workgroups>[,<latency us>]]]" (defaults 8 ranks, 32
+    workgroups, 10 us).  See :meth:`DataParallel._emulate`."""
+    if not spec:
+        return None
+    f = [float(v) for v in spec.split(",")]
+    f += [8, 32, 10][len(f) - 1:]
+    return {"busbw_GBps": f[0], "ranks": int(f[1]), "wgs": int(f[2]), "latency_us": f[3]}
+
+
+EMULATE = _parse_emulate(os.environ.get("DTG_COMM_EMULATE", ""))
+
+
 class _Bucket:
     __slots__ = ("group", "start", "end", "params", "pending", "work", "index")
 
@@ -55,6 +68,8 @@ class DataParallel:
         self._force = forced
         self._comm = True  # set_comm(False): gradients stay rank-local (bench.py's compute-only timing)
         self._cstreams = {}
+        self._estreams = {}
+        self.emulate = EMULATE if self.overlap else None
         self.buckets = []
         self._hooks = []
         cap = int(bucket_mb * (1 << 20))
@@ -110,12 +125,37 @@ class DataParallel:
                     ls.wait_stream(side)
                 with torch.cuda.stream(ls):
                     b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                self._emulate(v, ls)
                 return
             if side is not None:
                 # host-staged backends (gloo): the main stream waits for the side stream (an event, no host
                 # sync) and the collective is enqueued from the main stream exactly as without it
                 torch.cuda.current_stream(v.device).wait_stream(side)
             b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            self._emulate(v, torch.cuda.current_stream(v.device) if v.is_cuda else None)
+
+    def _emulate(self, v, after):
+        """DTG_COMM_EMULATE: make a one-card run pay what an N-rank RCCL all-reduce of this bucket costs the
+        chip.  A one-rank collective is a local copy that never waits on a peer, so it cannot show whether the
+        real one -- RCCL channel workgroups resident on CUs for the whole bus time, blocked on peers -- delays
+        the backward's remaining weight gradients (the overlap that decides 1->8 scaling).  After the real
+        collective is enqueued, a spin kernel (csrc/kernels/comm_emu.hip) holding ``wgs`` workgroups for
+        ``bytes * 2(N-1)/N / busbw + latency`` runs on a high-priority pool stream -- drawn from the same
+        torch stream pool, at the same priority, as the process group's collective stream -- after everything
+        the launching stream has queued; :meth:`finish` makes the main stream wait for it, as for the real
+        work.  Successive buckets serialise on that stream like collectives on RCCL's."""
+        e = self.emulate
+        if e is None or after is None:
+            return
+        from ..ops._native import lib
+        es = self._estreams.get(v.device.index)
+        if es is None:
+            es = self._estreams[v.device.index] = torch.cuda.Stream(device=v.device, priority=-1)
+        n = e["ranks"]
+        secs = v.numel() * v.element_size() * 2.0 * (n - 1) / n / (e["busbw_GBps"] * 1e9) + e["latency_us"] * 1e-6
+        es.wait_stream(after)
+        with torch.cuda.stream(es):
+            lib().comm_spin(secs, e["wgs"], 0)
 
     def _comm_stream(self, device):
         cs = self._cstreams.get(device.index)
@@ -158,6 +198,8 @@ class DataParallel:
                 self._launch(b)
         for b in self.buckets:
             b.work.wait()
+        for es in self._estreams.values():
+            torch.cuda.current_stream(es.device).wait_stream(es)
         self._reset()
 
     def set_comm(self, on):

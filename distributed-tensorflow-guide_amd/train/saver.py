@@ -247,8 +247,8 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
         arrays.append((n, _np_of(b)))
     if optimizer is not None:
         from ..parallel.flat import _view_like
-        # slots are stored in LOGICAL parameter order (round 3); older checkpoints held channels_last conv
-        # slots in physical [K,R,S,C] order under the same keys -- restore_flat converts those
+        # slots are stored in LOGICAL parameter order (since f74dff1); only the first checkpoints held
+        # channels_last conv slots in physical [K,R,S,C] order -- restore_flat(legacy_slot_layout=True)
         arrays.append((SLOT_LAYOUT_KEY, np.array(SLOT_LAYOUT_LOGICAL, dtype=np.int64)))
         arrays.append(("optimizer/step", np.array(int(getattr(optimizer, "step_count", 0)), dtype=np.int64)))
         for g in flat:
@@ -277,12 +277,22 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
     return prefix
 
 
-def restore_flat(flat, prefix, optimizer=None):
+def restore_flat(flat, prefix, optimizer=None, legacy_slot_layout=None):
     """Restore what :func:`save_flat` wrote.  With ``optimizer``: its slots too (created when the optimizer
-    has not stepped yet) and its step count.  Returns the checkpoint's global step (or None)."""
+    has not stepped yet) and its step count.  Returns the checkpoint's global step (or None).
+
+    Slots are read in logical parameter order, which every save_flat since f74dff1 writes -- with or without
+    the ``dtg/slot_layout`` marker (added later).  Only checkpoints from before f74dff1 hold channels_last
+    conv slots in physical [K,R,S,C] order; converting those is opt-in (``legacy_slot_layout=True`` or
+    ``DTG_LEGACY_SLOT_LAYOUT=1``), and refused for a checkpoint that carries the logical marker."""
     from ..parallel.flat import _view_like
     vals = read_tensors(prefix)
-    logical = int(vals.get(SLOT_LAYOUT_KEY, -1)) == SLOT_LAYOUT_LOGICAL
+    if legacy_slot_layout is None:
+        legacy_slot_layout = os.environ.get("DTG_LEGACY_SLOT_LAYOUT") == "1"
+    marked = int(vals.get(SLOT_LAYOUT_KEY, -1)) == SLOT_LAYOUT_LOGICAL
+    if legacy_slot_layout and marked:
+        raise ValueError("%s: legacy_slot_layout requested, but the checkpoint is marked logical" % prefix)
+    logical = not legacy_slot_layout
     with torch.no_grad():
         for g in flat:
             if optimizer is not None:  # slots present in the checkpoint but not yet allocated

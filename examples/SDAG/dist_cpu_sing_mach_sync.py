@@ -68,6 +68,7 @@ def main():
         print(r, gs, FLAGS.task_index)
         if is_chief:
             print(r, gs, FLAGS.task_index)
+            dtg.flags.sleep(FLAGS, 1)  # the chief paces an extra second (SDAG/dist_cpu_sing_mach_sync.py:111)
         dtg.flags.sleep(FLAGS, 1)
     print('Done', FLAGS.task_index)
     dtg.flags.sleep(FLAGS, 10)

@@ -67,6 +67,8 @@ def main():
     while not sess.should_stop():
         _, r, gs = sess.run([opt, c, global_step])
         print(r, 'step: ', gs, 'worker: ', FLAGS.task_index)
+        if is_chief:
+            dtg.flags.sleep(FLAGS, 1)  # the chief paces an extra second (ssgd.py:101 of the reference)
         dtg.flags.sleep(FLAGS, 1)
     print('Done', FLAGS.task_index)
     dtg.flags.sleep(FLAGS, 10)

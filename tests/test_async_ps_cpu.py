@@ -283,13 +283,16 @@ def test_async_ps_carries_bn_running_stats():
     assert (ps["n.running_var"] - 1).abs().max() > 1e-3
 
 
-def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeout=None, stall=None):
+def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeout=None, stall=None, env=None,
+               step_sleep=0.0):
     """Hogwild ranks with the worker-side options: overlapped pulls, a worker that dies (os._exit, no
-    finish) after ``die_after`` steps, a PS ``worker_timeout`` with a worker that stalls."""
+    finish) after ``die_after`` steps, a PS ``worker_timeout`` with a worker that stalls; ``env`` extra
+    environment (e.g. a short rank-liveness timeout), ``step_sleep`` seconds per worker step."""
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank))
+        os.environ.update(env or {})
         import time
         import dtg  # noqa: F401
         from dtg import ops
@@ -319,6 +322,8 @@ def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeo
                 loss = ops.softmax_cross_entropy(model(x), y)
                 loss.backward()
                 w.step_done()
+                if step_sleep:
+                    time.sleep(step_sleep)
                 if die_after is not None and rank == world - 1 and i + 1 == die_after:
                     q.put((rank, "ok", {"died": True}))
                     q.close()
@@ -392,6 +397,17 @@ def test_async_ps_survives_a_dead_worker():
     assert out[2] == {"died": True}
     assert out[0]["lost"] == [2]
     assert out[0]["per_worker"] == {1: 12, 2: 4} and out[0]["updates"] == 16
+
+
+def test_async_ps_dead_worker_outlives_rank_watchdog_timeout():
+    """comm.init starts the fail-stop rank watchdog (parallel/comm.py) for multi-rank jobs; an async-PS job
+    must not inherit it, or the PS and every survivor would exit (status 75) DTG_RANK_TIMEOUT after a
+    worker died.  Here the timeout is 1 s and the survivor keeps training ~4 s after the death."""
+    env = {"DTG_RANK_TIMEOUT": "1", "DTG_HEARTBEAT_S": "0.2"}
+    out = _run_opts(3, 24, die_after=2, env=env, step_sleep=0.2)
+    assert out[2] == {"died": True}
+    assert out[0]["lost"] == [2]
+    assert out[0]["per_worker"] == {1: 24, 2: 2} and out[1] == {"pushes": 24}
 
 
 def test_async_ps_worker_timeout_names_silent_workers():

@@ -15,6 +15,7 @@ import subprocess
 import sys
 import time
 
+import pytest
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -93,7 +94,9 @@ def test_killed_rank_then_resume_from_checkpoint(tmp_path):
     assert int(rd.get_tensor("global_step")) == 6 and int(rd.get_tensor("optimizer/step")) >= 4
 
 
-def test_restore_converts_legacy_physical_slots(tmp_path):
+def test_restore_slot_layouts(tmp_path):
+    """Marked logical, UNMARKED logical (every save_flat between f74dff1 and the marker) and -- opt-in only --
+    legacy physical [K,R,S,C] slots all restore to the same momentum."""
     import dtg  # noqa: F401
     from dtg.models.layers import Conv2d
     from dtg.optim import FusedSGD
@@ -116,11 +119,19 @@ def test_restore_converts_legacy_physical_slots(tmp_path):
     # forge a legacy checkpoint: no marker, slot in physical [K,R,S,C] order
     vals.pop("dtg/slot_layout")
     w = m[0].weight
+    write_tensors(str(tmp_path / "unmarked-1"), list(vals.items()))
     vals["0.weight/momentum"] = logical.permute(0, 2, 3, 1).contiguous().numpy()
     write_tensors(str(tmp_path / "legacy-1"), list(vals.items()))
-    for pref in (p, str(tmp_path / "legacy-1")):
+    for pref, legacy in ((p, None), (str(tmp_path / "unmarked-1"), None), (str(tmp_path / "legacy-1"), True)):
         m2, flat2 = build()
         opt2 = FusedSGD(flat2, lr=0.1, momentum=0.9)
-        assert restore_flat(flat2, pref, optimizer=opt2) == 1
+        assert restore_flat(flat2, pref, optimizer=opt2, legacy_slot_layout=legacy) == 1
         got = flat2.groups["compute"].state["momentum"]
         assert torch.equal(got[:w.numel()], mom[:w.numel()]), pref
+    # the default no longer scrambles an unmarked checkpoint: read as legacy it WOULD differ
+    m2, flat2 = build()
+    opt2 = FusedSGD(flat2, lr=0.1, momentum=0.9)
+    restore_flat(flat2, str(tmp_path / "unmarked-1"), optimizer=opt2, legacy_slot_layout=True)
+    assert not torch.equal(flat2.groups["compute"].state["momentum"][:w.numel()], mom[:w.numel()])
+    with pytest.raises(ValueError):
+        restore_flat(flat2, p, optimizer=opt2, legacy_slot_layout=True)

@@ -347,3 +347,28 @@ def test_emb_word_bwd_owned_matches_index_add():
     gw2 = g0.clone()
     lib().emb_word_bwd_owned(ds, ids, gw2)
     assert torch.equal(gw, gw2)  # deterministic
+
+
+@pytest.mark.parametrize("H", [768, 128])
+def test_scatter_rows_add_repeated_positions(H):
+    """heads.hip scatter_rows_add: positions repeated inside a sequence (padded masked_lm_positions are all 0)
+    accumulate every row -- the index_add_ semantics of the path it replaced -- against fp32 torch."""
+    L = lib()
+    B, S, P = 6, 32, 20
+    g = torch.Generator(device="cuda").manual_seed(0)
+    pos = torch.randint(0, S, (B, P), device="cuda", generator=g)
+    pos[:, P // 2:] = 0  # padded tail: all position 0
+    pos[1] = 3           # one sequence where every position is the same
+    dst = torch.randn(B * S, H, device="cuda", generator=g).bfloat16()
+    src = torch.randn(B * P, H, device="cuda", generator=g).bfloat16()
+    ref = dst.float().index_add(0, (torch.arange(B, device="cuda")[:, None] * S + pos).reshape(-1), src.float())
+    L.scatter_rows_add(dst, pos, src, S)
+    torch.cuda.synchronize()
+    err = (dst.float() - ref).abs().max().item()
+    assert err <= 0.05 * ref.abs().max().item(), err
+    cls = torch.randn(B, H, device="cuda", generator=g).bfloat16()
+    before = dst.float().clone()
+    L.scatter_rows_add(dst, None, cls, S)
+    exp = before.clone()
+    exp[torch.arange(B, device="cuda") * S] += cls.float()
+    assert (dst.float() - exp).abs().max().item() <= 0.05 * exp.abs().max().item()

@@ -36,6 +36,10 @@ for s in "$@"; do
     bench_pg_main) DTG_DDP_FORCE=1 DTG_WGRAD_STREAM=0 run bench_pg_main 600 python bench.py --steps 20 --warmup 5 ;;
     prof_pg) DTG_DDP_FORCE=1 run prof_pg 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pg -o run --output-format csv -- \
             python3 bench.py --steps 4 --warmup 3 ;;
+    test_launch) run pytest_launch 400 python -u -m pytest tests/test_launch_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    bench_emu) DTG_DDP_FORCE=1 DTG_COMM_EMULATE=${EMU:-100} run bench_emu 600 python bench.py --steps 20 --warmup 5 ;;
+    prof_emu) DTG_DDP_FORCE=1 DTG_COMM_EMULATE=${EMU:-100} run prof_emu 900 rocprofv3 --kernel-trace -d gpurun_out/prof_emu -o run \
+            --output-format csv -- python3 bench.py --steps 6 --warmup 3 ;;
     test_resnet) run pytest_resnet 900 python -u -m pytest tests/test_resnet_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
     kbench) run kbench 600 python tools/bench_kernels.py --json gpurun_out/kbench.json ;;
