@@ -19,10 +19,13 @@ workers intra-node (RCCL send/recv)").  Reference semantics kept:
 MI355X design:
 
 * **payloads** go over RCCL point-to-point: torch's RCCL process group gives every PS<->worker pair its
-  own 2-rank communicator and HIP stream, so the 7 pairs of a node move gradients and parameters
-  concurrently, each over its own xGMI link.  A push is one send per dtype group (bf16 compute grads,
-  fp32 norm/bias grads, the BN running-statistics delta); a pull is the bf16 compute mirror, the fp32
-  group and the module buffers.
+  own 2-rank communicator and HIP stream, so the pairs move gradients and parameters concurrently.  With
+  one process per GPU and every device visible to every process (examples/ResNet50/run_async.sh,
+  ``bench.py --mode async_ps``) each pair is a distinct GPU pair, which on MI355X's fully connected xGMI
+  mesh has a direct link of its own (7 per GPU); that the 7 transfers then run link-parallel has not been
+  traced on an 8-GPU node yet (the one-card rehearsals stage through host memory over gloo).  A push is one
+  send per dtype group (bf16 compute grads, fp32 norm/bias grads, the BN running-statistics delta); a pull
+  is the bf16 compute mirror, the fp32 group and the module buffers.
 * **request framing** goes over dtg's native TCP service (csrc/ps/server.cc, the same one the CPU PS
   uses): a worker enqueues a (rank, kind) token on one queue and the PS blocks in ``q_dequeue`` with
   the GIL released.  So the PS serves requests in arrival order with no busy spin and no device
@@ -483,8 +486,10 @@ class ElasticWorker:
 def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1):
     """Bootstrap the RCCL/gloo process group from a TF-style ClusterSpec: the PS task 0 is rank 0
     (its ``host:port`` + ``port_offset`` is the rendezvous), worker i is rank 1 + i.  One process per
-    GPU: pin each process to its GPU with HIP_VISIBLE_DEVICES (see examples/ResNet50/run_async.sh).
-    Returns (rank, world, device)."""
+    GPU: rank r uses device r % (visible devices), with every device left visible to every process
+    (examples/ResNet50/run_async.sh) -- RCCL can only use the direct xGMI peer links between GPUs a process
+    can see, so pinning each process to one device with HIP_VISIBLE_DEVICES would hide its peers.  On one
+    card (the gloo rehearsal) every rank lands on device 0.  Returns (rank, world, device)."""
     import datetime
     import os
 
@@ -497,7 +502,10 @@ def init_from_cluster(cluster, job_name, task_index, backend=None, port_offset=1
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     gloo_cuda = backend == "gloo" and os.environ.get("DTG_GLOO_DEVICE") == "cuda" and torch.cuda.is_available()
-    device = torch.device("cuda", 0) if backend == "nccl" or gloo_cuda else torch.device("cpu")
+    if backend == "nccl" or gloo_cuda:
+        device = torch.device("cuda", rank % max(1, torch.cuda.device_count()))
+    else:
+        device = torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     os.environ["MASTER_ADDR"] = "127.0.0.1" if ps_host in ("localhost", "") else ps_host

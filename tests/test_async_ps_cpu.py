@@ -7,6 +7,7 @@
 import os
 import sys
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -408,6 +409,24 @@ def test_async_ps_dead_worker_outlives_rank_watchdog_timeout():
     assert out[2] == {"died": True}
     assert out[0]["lost"] == [2]
     assert out[0]["per_worker"] == {1: 24, 2: 2} and out[1] == {"pushes": 24}
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_async_ps_one_ps_seven_workers(overlap):
+    """BASELINE.json config 4's topology, 1 PS + 7 workers (gloo on the CPU): every worker's pushes are all
+    applied (equal per-worker counts), nobody is lost, and the staleness stays within what a round-robin of 7
+    workers implies: a worker's pull is followed by at most the other 6 workers' updates before its push
+    (one exchange more with overlapped pulls)."""
+    steps = 6
+    out = _run_opts(8, steps, overlap=overlap)
+    ps = out[0]
+    assert ps["lost"] == []
+    assert ps["per_worker"] == {w: steps for w in range(1, 8)}
+    assert ps["updates"] == 7 * steps
+    st = ps["staleness"]
+    bound = 6 + (7 if overlap else 0)
+    assert max(st) <= 7 * 2 - 1 + (7 if overlap else 0)
+    assert sum(st) / len(st) <= bound, st
 
 
 def test_async_ps_worker_timeout_names_silent_workers():
