@@ -112,12 +112,17 @@ def main(argv=None):
 
     def train_step(forward_loss, dp, opt):
         """forward -> backward (bucketed all-reduce fired from inside) -> join -> fused apply, with roctx
-        ranges around each phase when DTG_TRACE=1 (dtg.utils.trace)"""
+        ranges around each phase when DTG_TRACE=1 (dtg.utils.trace).  The backward is seeded with a cached
+        1.0 (``loss.backward()`` would launch a framework fill kernel for it every step)."""
+        seed = []
+
         def step():
             with trace_range("dtg.forward"):
                 loss = forward_loss()
+            if not seed:
+                seed.append(torch.ones_like(loss))
             with trace_range("dtg.backward"):
-                loss.backward()
+                loss.backward(seed[0])
             with trace_range("dtg.allreduce.join"):
                 dp.finish()
             opt.step(grad_scale=dp.grad_scale)

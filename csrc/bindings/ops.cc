@@ -15,6 +15,13 @@ using dtg::bf16_t;
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// fp32 zeros on like's device, filled by a dtg kernel on the current stream
+at::Tensor zeros_f32(long long n, const at::Tensor& like) {
+  at::Tensor t = at::empty({n}, like.options().dtype(at::kFloat));
+  dtg::fill_zero(t.data_ptr(), n * 4, cur_stream());
+  return t;
+}
+
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
 #define CHECK_DT(x, dt) TORCH_CHECK((x).scalar_type() == (dt), #x " must be " #dt)
@@ -430,7 +437,7 @@ std::tuple<Tensor, Tensor> conv_fwd_c8(Tensor x, Tensor w, int64_t R, int64_t S,
   Tensor part;
   dtg::BnEpi bn;
   if (with_stats) {
-    part = at::zeros({(long long)dtg::kBnStatSlots * 2 * K}, x.options().dtype(at::kFloat));
+    part = zeros_f32((long long)dtg::kBnStatSlots * 2 * K, x);
     bn.part = part.data_ptr<float>();
     bn.mode = 1;
   } else {
@@ -448,12 +455,12 @@ std::tuple<Tensor, Tensor> conv_fwd_c8(Tensor x, Tensor w, int64_t R, int64_t S,
 constexpr int kPartRing = 16;
 constexpr long long kPartCap = (long long)dtg::kBnStatSlots * 2 * 2048;
 Tensor bn_part(const Tensor& like, int64_t C, bool pooled = false) {
-  if (!pooled || C > 2048) return at::zeros({(long long)dtg::kBnStatSlots * 2 * C}, like.options().dtype(at::kFloat));
+  if (!pooled || C > 2048) return zeros_f32((long long)dtg::kBnStatSlots * 2 * C, like);
   static Tensor* ring = new Tensor[64];  // per device; leaked on purpose (no teardown-order issues)
   static int next[64] = {0};
   const int dev = like.get_device();
   TORCH_CHECK(dev >= 0 && dev < 64, "device index");
-  if (!ring[dev].defined()) ring[dev] = at::zeros({kPartRing * kPartCap}, like.options().dtype(at::kFloat));
+  if (!ring[dev].defined()) ring[dev] = zeros_f32((long long)kPartRing * kPartCap, like);
   const int i = next[dev]++ % kPartRing;
   return ring[dev].narrow(0, i * kPartCap, (long long)dtg::kBnStatSlots * 2 * C);
 }
@@ -490,14 +497,24 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
                                    c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
                                    c10::optional<Tensor> invstd2, c10::optional<Tensor> part2,
                                    c10::optional<std::tuple<int64_t, int64_t>> sub2_hw,
-                                   c10::optional<Tensor> xcoef) {
+                                   c10::optional<Tensor> xcoef, c10::optional<Tensor> a2,
+                                   c10::optional<Tensor> colbias) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
   CHECK_DT(B, at::kBFloat16);
   TORCH_CHECK(mode >= 1 && mode <= 3, "mode in {1, 2, 3}");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && B.stride(1) == 1, "2-D operands, contiguous rows");
-  const int M = (int)A.size(0), K = (int)A.size(1);
+  const bool two = a2.has_value() && a2->defined();
+  const int M = (int)A.size(0), K = (int)A.size(1) + (two ? (int)a2->size(1) : 0);
+  if (two) {  // BN-folded dgrad: A operand = [A | a2] along K (BnEpi::a2)
+    TORCH_CHECK(mode == 3, "a2 (K-concatenated A) is mode 3 only");
+    CHECK_IN(*a2);
+    CHECK_DT(*a2, at::kBFloat16);
+    TORCH_CHECK(a2->dim() == 2 && a2->size(0) == M && A.size(1) % 64 == 0 && a2->size(1) % 8 == 0,
+                "a2 must be [M, K2] with the first part's K a multiple of 64");
+    TORCH_CHECK(((uintptr_t)a2->data_ptr() % 16) == 0 && a2->stride(0) % 8 == 0, "a2: 16-byte aligned rows");
+  }
   const int N = (int)(mode == 1 ? B.size(0) : B.size(1));
   TORCH_CHECK((mode == 1 ? B.size(1) : B.size(0)) == K, "gemm_bn K mismatch");
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0 && B.stride(0) % 8 == 0, "K, N and row strides must be multiples of 8");
@@ -567,6 +584,18 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
       bn.xcoef = xcoef->data_ptr<float>();
       bn.xc_n = K;
     }
+  }
+  if (two) {
+    bn.a2 = cbfp(*a2);
+    bn.lda2 = a2->stride(0);
+    bn.ka1 = (int)A.size(1);
+  }
+  if (colbias.has_value() && colbias->defined()) {
+    TORCH_CHECK(mode == 3, "colbias is mode 3 only");
+    CHECK_IN(*colbias);
+    CHECK_DT(*colbias, at::kFloat);
+    TORCH_CHECK(colbias->numel() == N && ((uintptr_t)colbias->data_ptr() % 16) == 0, "colbias must be [N] fp32");
+    bn.colbias = colbias->data_ptr<float>();
   }
   dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(o), N, M, N, K, bt, bn, cur_stream());
   return {o, part};
@@ -890,6 +919,60 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
                   ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw);
 }
 
+// BN backward in two halves (the BN-folded 1x1 dgrads, models/resnet_fused.py): the finalize of the epilogue
+// partials -> coef [a, bx, c] (dx = a*dp + bx*x + c) and dgamma/dbeta accumulated ...
+Tensor bn_bwd_coef(Tensor part, Tensor gamma, Tensor smean, Tensor sinv, Tensor dgamma_acc, Tensor dbeta_acc, int64_t M) {
+  CHECK_IN(part);
+  CHECK_DT(part, at::kFloat);
+  const int C = (int)gamma.numel();
+  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
+  for (const Tensor* t : {&gamma, &smean, &sinv, &dgamma_acc, &dbeta_acc}) {
+    CHECK_IN(*t);
+    CHECK_DT(*t, at::kFloat);
+    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
+  }
+  c10::DeviceGuard dg(part.device());
+  auto coef = at::empty({3LL * C}, part.options());
+  dtg::bn_bwd_coef_from_part(part.data_ptr<float>(), gamma.data_ptr<float>(), smean.data_ptr<float>(),
+                             sinv.data_ptr<float>(), coef.data_ptr<float>(), dgamma_acc.data_ptr<float>(),
+                             dbeta_acc.data_ptr<float>(), M, C, 1, cur_stream());
+  return coef;
+}
+
+// ... and the dx pass from those coefficients
+Tensor bn_dx_coef(Tensor dp, Tensor x, Tensor coef) {
+  CHECK_IN(dp);
+  CHECK_IN(x);
+  CHECK_DT(dp, at::kBFloat16);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && dp.sizes() == x.sizes() && x.size(1) % 8 == 0, "dp/x must be [M, C]");
+  CHECK_IN(coef);
+  CHECK_DT(coef, at::kFloat);
+  TORCH_CHECK(coef.numel() == 3 * x.size(1), "coef must be [3C]");
+  c10::DeviceGuard dg(x.device());
+  auto dx = at::empty_like(x);
+  dtg::bn_dx_from_coef(cbfp(dp), cbfp(x), coef.data_ptr<float>(), bfp(dx), nullptr, x.size(0), (int)x.size(1),
+                       cur_stream());
+  return dx;
+}
+
+// W [K, N] (a 1x1 conv weight [Cout, Cin] read as the dgrad's B operand) -> (Wab [2K, N] bf16, cw [N] fp32)
+std::tuple<Tensor, Tensor> bn_fold_weights(Tensor W, Tensor coef) {
+  CHECK_CUDA(W);
+  CHECK_DT(W, at::kBFloat16);
+  TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1, "W must be [K, N] with contiguous rows");
+  const int K = (int)W.size(0), N = (int)W.size(1);
+  CHECK_IN(coef);
+  CHECK_DT(coef, at::kFloat);
+  TORCH_CHECK(coef.numel() == 3LL * K, "coef must be [3K]");
+  c10::DeviceGuard dg(W.device());
+  auto Wab = at::empty({2LL * K, N}, W.options());
+  auto cw = at::empty({N}, coef.options());
+  dtg::bn_fold_weights(cbfp(W), W.stride(0), coef.data_ptr<float>(), bfp(Wab), cw.data_ptr<float>(), K, N,
+                       cur_stream());
+  return {Wab, cw};
+}
+
 }  // namespace
 
 void register_transformer_ops(pybind11::module_& m);  // transformer_ops.cc
@@ -911,7 +994,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false,
         pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none(),
         pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none(),
-        pybind11::arg("sub2_hw") = pybind11::none(), pybind11::arg("xcoef") = pybind11::none());
+        pybind11::arg("sub2_hw") = pybind11::none(), pybind11::arg("xcoef") = pybind11::none(),
+        pybind11::arg("a2") = pybind11::none(), pybind11::arg("colbias") = pybind11::none());
   m.def("bn_finalize", &bn_finalize, pybind11::arg("part"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("M"), pybind11::arg("momentum"),
         pybind11::arg("eps"));
@@ -939,6 +1023,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("bits") = pybind11::none());
   m.def("bn_bwd_part", &bn_bwd_part);
+  m.def("bn_bwd_coef", &bn_bwd_coef);
+  m.def("bn_dx_coef", &bn_dx_coef);
+  m.def("bn_fold_weights", &bn_fold_weights);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);
   m.def("momentum_apply", &momentum_apply);
@@ -948,6 +1035,37 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_spin", [](double seconds, int64_t wgs, int64_t lds_bytes) {
     dtg::comm_spin(seconds, (int)wgs, (int)lds_bytes, cur_stream());
   }, pybind11::arg("seconds"), pybind11::arg("wgs") = 32, pybind11::arg("lds_bytes") = 0);
+  m.def("hyper_tick", [](Tensor hyper) {
+    check_hyper(hyper);
+    c10::DeviceGuard dg(hyper.device());
+    dtg::hyper_tick(hyper.data_ptr<float>(), cur_stream());
+  });
+  m.def("stem_pack_weights", [](Tensor w) {
+    CHECK_CUDA(w);
+    CHECK_DT(w, at::kBFloat16);
+    TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(1) <= 4,
+                "w: channels_last [K, C<=4, R, S]");
+    const int K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3), S2 = (S + 1) / 2;
+    const int KP = (R * S2 * 8 + 63) / 64 * 64;
+    c10::DeviceGuard dg(w.device());
+    auto wp = at::empty({K, KP}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    dtg::stem_pack_weights(cbfp(w), bfp(wp), K, C, R, S, S2, KP, cur_stream());
+    return wp;
+  });
+  m.def("stem_dw_add", [](Tensor src, Tensor grad, bool pair) {
+    // src [K, R, S2, 8] fp32 (pair) or [K, R, S, 8]; grad: the channels_last [K, C, R, S] parameter gradient
+    CHECK_IN(src);
+    CHECK_DT(src, at::kFloat);
+    CHECK_CUDA(grad);
+    TORCH_CHECK(grad.dim() == 4 && grad.is_contiguous(at::MemoryFormat::ChannelsLast), "grad: channels_last [K,C,R,S]");
+    TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16, "grad fp32/bf16");
+    const int K = grad.size(0), C = grad.size(1), R = grad.size(2), S = grad.size(3);
+    TORCH_CHECK(src.dim() == 4 && src.size(0) == K && src.size(1) == R && src.size(3) == 8 && C <= 4 &&
+                    src.size(2) == (pair ? (S + 1) / 2 : S), "stem dw source shape");
+    c10::DeviceGuard dg(grad.device());
+    dtg::stem_dw_add(src.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kBFloat16, K, R, S, C,
+                     (int)src.size(2), pair ? 1 : 0, cur_stream());
+  });
   m.def("launch_probe", [](int64_t grid, int64_t lds_bytes) {
     dtg::launch_probe((int)grid, (int)lds_bytes, cur_stream());
   });

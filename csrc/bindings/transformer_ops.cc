@@ -373,11 +373,12 @@ bool emb_word_bwd_owned(Tensor ds, Tensor ids, Tensor gW) {
   return true;
 }
 
-// stream-ordered zero fill (hipMemsetAsync: a DMA fill, no framework kernel)
+// stream-ordered zero fill on a dtg kernel (no framework or runtime fill kernel)
 void zero_(Tensor t) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() % 16) == 0, "zero_: 16-byte aligned tensor");
   c10::DeviceGuard dg(t.device());
-  C10_HIP_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()));
+  dtg::fill_zero(t.data_ptr(), t.numel() * t.element_size(), cur_stream());
 }
 
 void register_transformer_ops(py::module_& m) {

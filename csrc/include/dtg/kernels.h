@@ -22,6 +22,9 @@ void adam_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* m, f
                 hipStream_t st);
 void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st);
 void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
+void hyper_tick(float* hyper, hipStream_t st);
+// zero `bytes` bytes at p (16-B aligned for the vector part) with a dtg kernel
+void fill_zero(void* p, long long bytes, hipStream_t st);
 
 // ---- emulated blocking collective (comm_emu.hip; parallel/ddp.py DTG_COMM_EMULATE) ------------------
 void comm_spin(double seconds, int wgs, int lds_bytes, hipStream_t st);
@@ -65,6 +68,13 @@ struct BnEpi {
   // written to memory (gemm_bf16_bn mode 1: the A operand, c = k; gemm_bf16_xb: the B operand, c = column)
   const float* xcoef = nullptr;
   int xc_n = 0;
+  // mode 3/4, optional (BN-folded dgrad): the A operand is the K-concatenation [A | a2] -- columns k < ka1 from
+  // A, k >= ka1 from a2 (same rows, row stride lda2; ka1 % 64 == 0) -- and colbias[n] is added to every
+  // accumulator before the relu mask / residual add (batchnorm.hip bn_fold_weights)
+  const bf16_t* a2 = nullptr;
+  long long lda2 = 0;
+  int ka1 = 0;
+  const float* colbias = nullptr;
 };
 
 // host: fill the old_sub2 fields of a BnEpi for an H x W image
@@ -106,6 +116,13 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
                        const float* smean2, const float* sinv2, bf16_t* dx, bf16_t* dx2, float* dgamma, float* dbeta,
                        float* dgamma2, float* dbeta2, float* ws, long long M, int C, int accum, hipStream_t st);
 // finish a backward BN from mode-2 partials: dx = a*dp + bx*x + c0 (ws: 3C floats), dres = dp if given
+void bn_bwd_coef_from_part(const float* part, const float* gamma, const float* smean, const float* sinv, float* coef,
+                           float* dgamma, float* dbeta, long long M, int C, int accum, hipStream_t st);
+void bn_dx_from_coef(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_t* dx, bf16_t* dres, long long M, int C,
+                     hipStream_t st);
+// Wab = [diag(a) W ; diag(bx) W] ([2K][N] bf16), cw = c^T W ([N] fp32) for coef = [a, bx, c] (batchnorm.hip)
+void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
+                     hipStream_t st);
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
                       int C, int accum, hipStream_t st);
@@ -219,6 +236,11 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                       float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
                       int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st);
 long long stem_bwd_workspace_floats(long long M, int C);
+// channels_last [K, C, R, S] stem weights -> pixel-pair form [K][KP] (KP >= R * S2 * 8, zero padded)
+void stem_pack_weights(const bf16_t* w, bf16_t* wp, int K, int C, int R, int S, int S2, int KP, hipStream_t st);
+// grad[K,R,S,C] (+)= the stem conv's padded-channel weight gradient (pair form: [K,R,S2,8], else [K,R,S,8])
+void stem_dw_add(const float* src, void* grad, int grad_bf16, int K, int R, int S, int C, int S2, int pair,
+                 hipStream_t st);
 // x [N,H,W,C<=4] -> xp [N, H+2*pad, Wp, 4], zero padded (the pixel-pair stem conv's input)
 void stem_pack_pairs(const bf16_t* x, bf16_t* xp, int N, int H, int W, int C, int pad, int Hp, int Wp,
                      hipStream_t st);

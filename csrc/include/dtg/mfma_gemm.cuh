@@ -97,6 +97,27 @@ struct DenseKC {
     return sel(k < K, p + (long long)r * ld + k);
   }
 };
+// KC operand concatenated along K from two matrices with the same rows: k < K1 from p, k >= K1 from p2 (K1 a
+// multiple of the 64-deep K-step, so a step never straddles the two and the pick is wave-uniform)
+template <bool GUARD>
+struct DenseKC2 {
+  static constexpr bool kGuard = GUARD;
+  const bf16_t* p;
+  long long ld;
+  int rows, K;
+  const bf16_t* p2;
+  long long ld2;
+  int K1;
+  __device__ __forceinline__ const void* chunk(int row, int k) const {
+    const bool second = k >= K1;
+    const bf16_t* base = second ? p2 : p;
+    const long long l = second ? ld2 : ld;
+    const int kk = second ? k - K1 : k;
+    if constexpr (!GUARD) return base + (long long)row * l + kk;
+    const int r = row < rows ? row : rows - 1;
+    return sel(k < K, base + (long long)r * l + kk);
+  }
+};
 // MC: matrix stored [K][ld] with the row/col (M or N) index contiguous
 template <bool GUARD>
 struct DenseMC {

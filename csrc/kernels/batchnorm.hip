@@ -510,15 +510,22 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
 }
 
 // Backward from mode-2 epilogue partials: dp is already relu-masked, so the dx pass reads dp and x.
-void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
-                      const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
-                      int C, int accum, hipStream_t st) {
-  const BnGeom g = bn_geom(M, C);
+// Two halves, also callable on their own (the BN-folded 1x1 dgrads, models/resnet_fused.py): the finalize
+// turns the partials into dgamma / dbeta and coef = [a, bx, c] with dx = a*dp + bx*x + c per channel ...
+void bn_bwd_coef_from_part(const float* part, const float* gamma, const float* smean, const float* sinv, float* coef,
+                           float* dgamma, float* dbeta, long long M, int C, int accum, hipStream_t st) {
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
                                                     nullptr, const_cast<float*>(smean), const_cast<float*>(sinv), 0.f,
-                                                    0.f, ws, dgamma, dbeta, 1); DTG_LAUNCH_CHECK();
+                                                    0.f, coef, dgamma, dbeta, 1); DTG_LAUNCH_CHECK();
+}
+
+// ... and the dx pass applies them (one read of dp and x, one write of dx; dres: a copy of dp)
+void bn_dx_from_coef(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_t* dx, bf16_t* dres, long long M, int C,
+                     hipStream_t st) {
+  const BnGeom g = bn_geom(M, C);
   const long long rpa = elementwise_rpc(g, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
+  const float* ws = coef;
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
     if (!bn_nt_loads()) {  // DTG_BN_NT=0: plain loads (A/B)
       if (dres) { bn_bwd_dx_kernel<T, false, true, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
@@ -527,6 +534,39 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
                                                                                       rpa); DTG_LAUNCH_CHECK(); }
     else { bn_bwd_dx_kernel<T, false, false, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
   }));
+}
+
+void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
+                      const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
+                      int C, int accum, hipStream_t st) {
+  bn_bwd_coef_from_part(part, gamma, smean, sinv, ws, dgamma, dbeta, M, C, accum, st);
+  bn_dx_from_coef(dp, x, ws, dx, dres, M, C, st);
+}
+
+// BN backward folded into the following 1x1 data gradient.  With dy = a*dp + bx*x + c per channel k (coef),
+//   dx[p, n] = sum_k dy[p, k] W[k, n] = sum_k dp[p, k] (a_k W[k, n]) + sum_k x[p, k] (bx_k W[k, n]) + sum_k c_k W[k, n]
+// so the dgrad is ONE GEMM over the K-concatenation [dp | x] with the weights [diag(a) W ; diag(bx) W] (rounded to
+// bf16 once here) plus the constant row cw = c^T W (fp32, added in the epilogue) -- no dx pass over HBM.
+// W [K][N] (row stride ldw); Wab [2K][N] contiguous.  One thread per column n, rows in order: coalesced rows,
+// deterministic column sums.
+__global__ void __launch_bounds__(256) bn_fold_weights_kernel(const bf16_t* __restrict__ W, long long ldw,
+                                                              const float* __restrict__ coef, bf16_t* __restrict__ Wab,
+                                                              float* __restrict__ cw, int K, int N) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float w = bf2f(W[(long long)k * ldw + n]);
+    Wab[(long long)k * N + n] = f2bf(coef[k] * w);
+    Wab[(long long)(K + k) * N + n] = f2bf(coef[K + k] * w);
+    s = fmaf(coef[2 * K + k], w, s);
+  }
+  cw[n] = s;
+}
+
+void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
+                     hipStream_t st) {
+  bn_fold_weights_kernel<<<(N + 255) / 256, 256, 0, st>>>(W, ldw, coef, Wab, cw, K, N); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

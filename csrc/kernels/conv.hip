@@ -520,7 +520,7 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
     }
   if (empty && bn.mode != 0) return 0;  // rows no launch writes would be missing from the statistics
   if (empty && beta == 0.f && zero_rest) {  // residue classes no tap reaches are zero
-    DTG_HIP_CHECK(hipMemsetAsync(dx, 0, (size_t)G.N * G.H * G.W * G.C * sizeof(bf16_t), st));
+    fill_zero(dx, (long long)G.N * G.H * G.W * G.C * sizeof(bf16_t), st);
     beta = 1.f;
   }
   Epi e{dx, G.C, 1, 1.f, beta, nullptr, 0};

@@ -92,10 +92,19 @@ long long gemm_workspace_floats(int M, int N, int K, int split_k) {
 
 static bool skinny(int N) { return N <= 64; }
 
+// DTG_WGRAD8=1 (experiment): weight gradients (both operands MN-contiguous, M and N multiples of 256) on the
+// 256x256 8-wave kernel (gemm8.hip), split-K sized for its tiles
+static bool wgrad8() {
+  static const bool on = getenv("DTG_WGRAD8") && getenv("DTG_WGRAD8")[0] == '1';
+  return on;
+}
+static bool wgrad8_shape(int M, int N, int a_kc) { return wgrad8() && !a_kc && M % 256 == 0 && N % 256 == 0; }
+
 static bool short_m(int M, int N) { return M <= 64 && N >= 128; }
 
 int gemm_pick_split(int M, int N, int K, int a_kc, int target_wgs) {
-  const int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
+  int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
+  if (wgrad8_shape(M, N, a_kc)) BMv = BNv = 256;
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   // forward / data-gradient GEMMs (K-contiguous A) with >= 128 tiles: the fp32 partial round trip
   // costs more than the idle CUs do (BERT 8192x768x3072: 47 us unsplit, 56 us split 2;
@@ -248,6 +257,10 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
     return;
   }
+  if (bt.count == 1 && !b_kc && wgrad8_shape(M, N, a_kc)) {
+    gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
+    return;
+  }
   if (split_k > 1 || !a_kc) {
     // weight gradients (MN-contiguous A, split-K over the token/pixel dimension): the single-stage
     // 128x128 ring beat every other tile and the 2-stage ring on all of them, BERT's 768x3072x8192
@@ -295,11 +308,21 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 template <class CF, int MODE, bool GUARD, bool PF, int XF = 0>
 static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                       const Epi& e, const BnEpi& bn, hipStream_t st) {
-  using SA = DenseKC<GUARD>;
   using SB = std::conditional_t<MODE == 1, DenseKC<GUARD>, DenseMC<GUARD>>;
-  SA sa{A, lda, M, K};
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
+  if constexpr (MODE == 3 || MODE == 4) {
+    if (bn.a2) {  // BN-folded dgrad: A = [A | a2] along K
+      using SA2 = DenseKC2<GUARD>;
+      SA2 sa{A, lda, M, K, bn.a2, bn.lda2, bn.ka1};
+      hipLaunchKernelGGL((gemm_kernel<CF, true, false, SA2, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
+                         dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
+      DTG_LAUNCH_CHECK();
+      return;
+    }
+  }
+  using SA = DenseKC<GUARD>;
+  SA sa{A, lda, M, K};
   hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
                      dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn); DTG_LAUNCH_CHECK();
 }

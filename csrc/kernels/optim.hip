@@ -219,4 +219,31 @@ void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st) {
   f32_to_bf16_kernel<<<grid_for((n >> 3) + 1, 256, 2048), 256, 0, st>>>(x, y, n); DTG_LAUNCH_CHECK();
 }
 
+// Stream-ordered zero fill with vector stores (instead of hipMemsetAsync, which launches the runtime's own
+// fill kernel): 16 B per lane, then the byte tail.
+__global__ void __launch_bounds__(256) fill_zero_kernel(unsigned char* __restrict__ p, long long bytes) {
+  const long long nvec = bytes >> 4;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride)
+    reinterpret_cast<uint4*>(p)[v] = make_uint4(0u, 0u, 0u, 0u);
+  if (blockIdx.x == 0)
+    for (long long i = (nvec << 4) + threadIdx.x; i < bytes; i += blockDim.x) p[i] = 0;
+}
+
+void fill_zero(void* p, long long bytes, hipStream_t st) {
+  if (bytes <= 0) return;
+  fill_zero_kernel<<<grid_for((bytes >> 4) + 1, 256, 4096), 256, 0, st>>>(reinterpret_cast<unsigned char*>(p), bytes);
+  DTG_LAUNCH_CHECK();
+}
+
+// hyper[1] += 1: the step counter the applies read (device-resident so a captured step replays with a fresh
+// value); one lane, one vector store, stream-ordered before the step's apply kernels
+__global__ void hyper_tick_kernel(float* hyper) {
+  if (threadIdx.x == 0) hyper[1] = hyper[1] + 1.f;
+}
+
+void hyper_tick(float* hyper, hipStream_t st) {
+  hyper_tick_kernel<<<1, 64, 0, st>>>(hyper); DTG_LAUNCH_CHECK();
+}
+
 }  // namespace dtg

@@ -493,7 +493,7 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
   if (stem_band_ok(H, C, k, s, pad, P, Q) && bg.nchunk >= kBnStatSlots) {
     const size_t lds = stem_band_lds(Q, C);
     const unsigned nb = (unsigned)(N * (H / kStemBandRows));
-    DTG_HIP_CHECK(hipMemsetAsync(part, 0, (size_t)kBnStatSlots * 2 * C * sizeof(float), st));
+    fill_zero(part, (long long)kBnStatSlots * 2 * C * sizeof(float), st);
     hipLaunchKernelGGL(stem_bwd_band_kernel<false>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
                        sinv, nullptr, g, part, nullptr); DTG_LAUNCH_CHECK();
     bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr,
@@ -513,6 +513,61 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
   dim3 ga((unsigned)((M + rpa - 1) / rpa), bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_dx_kernel<T><<<ga, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, coef, g, M,
                                                                    rpa, dy)); DTG_LAUNCH_CHECK();
+}
+
+// Stem weight gradient from the padded-channel wgrad layouts into the parameter's own [K, R, S, C] memory
+// (channels_last [K, C, R, S]): grad[k, r, s, c] += src[k, r, s', 8-chunk]; pair form (the pixel-pair conv,
+// ops/conv.py stem_pairs): s' = s / 2, lane (s % 2) * 4 + c of a [K, R, S2, 8] buffer; plain form: s' = s,
+// lane c of [K, R, S, 8].  One pass replaces a fill, a permuted copy, a cast and an add.
+template <bool GBF16>
+__global__ void __launch_bounds__(256) stem_dw_add_kernel(const float* __restrict__ src, void* __restrict__ grad, int K,
+                                                          int R, int S, int C, int S2, int pair) {
+  const int total = K * R * S * C;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = i % C, s = (i / C) % S, r = (i / (C * S)) % R, k = i / (C * S * R);
+    const int sp = pair ? s / 2 : s, lane = pair ? (s & 1) * 4 + c : c;
+    const float v = src[((long long)(k * R + r) * S2 + sp) * 8 + lane];
+    if constexpr (GBF16) {
+      bf16_t* g = reinterpret_cast<bf16_t*>(grad);
+      g[i] = f2bf(bf2f(g[i]) + v);
+    } else {
+      float* g = reinterpret_cast<float*>(grad);
+      g[i] += v;
+    }
+  }
+}
+
+void stem_dw_add(const float* src, void* grad, int grad_bf16, int K, int R, int S, int C, int S2, int pair,
+                 hipStream_t st) {
+  const int total = K * R * S * C;
+  const int grid = (total + 255) / 256;
+  if (grad_bf16) stem_dw_add_kernel<true><<<grid, 256, 0, st>>>(src, grad, K, R, S, C, S2, pair);
+  else stem_dw_add_kernel<false><<<grid, 256, 0, st>>>(src, grad, K, R, S, C, S2, pair);
+  DTG_LAUNCH_CHECK();
+}
+
+// Pixel-pair stem weights (ops/conv.py stem_pairs): w [K, C, R, S] in channels_last memory ([K][R][S][C]) ->
+// wp [K][KP] bf16, column (r, s2, lane) = r * S2 * 8 + s2 * 8 + lane with lane = (s % 2) * 4 + c, s = 2 s2 + s % 2;
+// taps s >= S, channels c >= C and the columns past R * S2 * 8 are zero.  One pass per step instead of a pad /
+// permute / pad chain of framework kernels.
+__global__ void __launch_bounds__(256) stem_pack_weights_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wp,
+                                                                int K, int C, int R, int S, int S2, int KP) {
+  const int total = K * KP;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int k = i / KP, j = i % KP;
+    bf16_t v = 0;
+    if (j < R * S2 * 8) {
+      const int r = j / (S2 * 8), rem = j % (S2 * 8), lane = rem & 7;
+      const int s = (rem >> 3) * 2 + (lane >> 2), c = lane & 3;
+      if (s < S && c < C) v = w[((long long)(k * R + r) * S + s) * C + c];
+    }
+    wp[i] = v;
+  }
+}
+
+void stem_pack_weights(const bf16_t* w, bf16_t* wp, int K, int C, int R, int S, int S2, int KP, hipStream_t st) {
+  const int total = K * KP;
+  stem_pack_weights_kernel<<<(total + 255) / 256, 256, 0, st>>>(w, wp, K, C, R, S, S2, KP); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -67,6 +67,11 @@ _SUB2 = os.environ.get("DTG_DGRAD_SUB2", "1") != "0"
 # 14.46k vs 14.80k img/s -- the prologue costs the forward GEMMs +0.39 ms and the weight gradients +1.2 ms
 # per step against the 0.55 ms apply pass it removes (profiles/r03_bn2_prologue).
 _BN2X = os.environ.get("DTG_BN2_FUSE", "0") == "1"
+# DTG_BN_FOLD=1: BN3 (identity blocks) and BN1 backward folded into the following 1x1 dgrad -- the dgrad GEMM
+# reads [dp | y] along K against [diag(a) W ; diag(bx) W] plus the constant row c^T W (dy = a*dp + bx*y + c), so the
+# main stream makes no dx pass for them; the weight gradient, which needs dy itself, gets it from a dx pass on the
+# side stream (batchnorm.hip bn_fold_weights, gemm_bn(a2=..., colbias=...)).  Needs _FUSE and _LINK.
+_FOLD = os.environ.get("DTG_BN_FOLD", "0") == "1"
 
 
 class _Bn3Link:
@@ -232,6 +237,7 @@ class _BottleneckFn(torch.autograd.Function):
         # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
         lk = ctx.link_out
         dyd = None
+        coef3 = None  # set when BN3's backward is folded into the conv3 dgrad (_FOLD)
         if (lk is not None and lk.part is not None and do.data_ptr() == lk.dp.data_ptr()
                 and do.shape == lk.dp.shape):
             # block i+1 already masked dL/d out (do is dp) and reduced this BN's statistics
@@ -240,6 +246,8 @@ class _BottleneckFn(torch.autograd.Function):
                 dy3, dyd = L.bn_bwd2_part(do, y3, lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)],
                                           sv[13], lk.part2, bd.weight, sv[14], sv[15], g[id(bd.weight)],
                                           g[id(bd.bias)])
+            elif _FOLD and bits12_ok(ctx):
+                coef3 = L.bn_bwd_coef(lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)], y3.shape[0])
             else:
                 dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
             dres = do  # our own buffer (pointer-checked above): dx accumulates into it in place
@@ -254,7 +262,11 @@ class _BottleneckFn(torch.autograd.Function):
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
         bits1, bits2 = ctx.bits12 if _FUSE else (None, None)
         ctx.bits12 = None
-        if _FUSE and bits2 is not None:  # relu mask from the forward's bits: mode 3 with nothing to accumulate
+        if coef3 is not None:  # BN3 folded: A = [dp3 | y3], B = [diag(a) W3 ; diag(bx) W3], + c^T W3
+            w3ab, cw3 = L.bn_fold_weights(_mat(w3), coef3)
+            dp2, q2 = L.gemm_bn(do, w3ab, 3, y2, m2, i2, b2.weight, b2.bias, mask=bits2, pooled=True, a2=y3,
+                                colbias=cw3)
+        elif _FUSE and bits2 is not None:  # relu mask from the forward's bits: mode 3 with nothing to accumulate
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 3, y2, m2, i2, b2.weight, b2.bias, mask=bits2, pooled=True)
         elif _FUSE:
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
@@ -265,6 +277,9 @@ class _BottleneckFn(torch.autograd.Function):
         if coef2 is not None:  # conv3's input is relu(bn2(y2)), applied in the weight-gradient GEMM's prologue
             with overlap.wgrad_scope(dy3, y2, coef2):
                 _wgrad(dy3, y2, g[id(w3)].view(cout, width), coef2)
+        elif coef3 is not None:
+            with overlap.wgrad_scope(do, y3, coef3, a2):  # dy3 for the weight gradient only, off the main stream
+                _wgrad(L.bn_dx_coef(do, y3, coef3), a2, g[id(w3)].view(cout, width))
         else:
             with overlap.wgrad_scope(dy3, a2):
                 _wgrad(dy3, a2, g[id(w3)].view(cout, width))
@@ -283,16 +298,19 @@ class _BottleneckFn(torch.autograd.Function):
         with overlap.wgrad_scope(dy2_4, a1):
             _conv_wgrad(dy2_4, a1.view(n, h, w, width), g[id(w2)].permute(0, 2, 3, 1), st, 1)
         # BN1 + conv1 (1x1): its dgrad accumulates into the identity-branch gradient
-        if _FUSE:
-            dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
-        else:
-            dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         dx_done = False
         sub2_hw = None
         lk_in = ctx.link_in
         ctx.link_in = None
         if lk_in is not None and lk_in.y3.shape != x2.shape:
             lk_in = None
+        coef1 = dy1 = None
+        if _FUSE and _FOLD and lk_in is not None and bits12_ok(ctx):  # folded into the mode-3 conv1 dgrad below
+            coef1 = L.bn_bwd_coef(q1, b1.weight, m1, i1, g[id(b1.weight)], g[id(b1.bias)], y1.shape[0])
+        elif _FUSE:
+            dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
+        else:
+            dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         if blk.down is not None:
             yd, md, idd = sv[13:16]
             bd, wd = blk.down.bn, blk.down.conv.weight
@@ -326,15 +344,25 @@ class _BottleneckFn(torch.autograd.Function):
             if lk_in is not None:  # mode 3: finish the previous block's BN3 reduction in this epilogue
                 part2 = None
                 if lk_in.yd is not None:  # the previous block is a projection block: its shortcut BN too
-                    part2 = L.bn_part_alloc(dy1, c, pooled=True)
-                _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                    mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
-                                    invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw)
+                    part2 = L.bn_part_alloc(dp1, c, pooled=True)
+                if coef1 is not None:  # BN1 folded: A = [dp1 | y1] against [diag(a) W1 ; diag(bx) W1], + c^T W1
+                    w1ab, cw1 = L.bn_fold_weights(_mat(w1), coef1)
+                    _, part = L.gemm_bn(dp1, w1ab, 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
+                                        mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
+                                        invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw, a2=y1, colbias=cw1)
+                else:
+                    _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
+                                        mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
+                                        invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw)
                 lk_in.part, lk_in.part2, lk_in.dp = part, part2, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
-        with overlap.wgrad_scope(dy1, x2):
-            _wgrad(dy1, x2, g[id(w1)].view(width, c))
+        if coef1 is not None:
+            with overlap.wgrad_scope(dp1, y1, coef1, x2):  # dy1 for the weight gradient only, off the main stream
+                _wgrad(L.bn_dx_coef(dp1, y1, coef1), x2, g[id(w1)].view(width, c))
+        else:
+            with overlap.wgrad_scope(dy1, x2):
+                _wgrad(dy1, x2, g[id(w1)].view(width, c))
         if not all(direct for _, direct in accs):
             overlap.sync_current(x2.device)  # side-stream wgrads land in these before autograd adds them
         grads = []
@@ -345,6 +373,11 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 grads.append(a.to(p.dtype))
         return (dx2.view(n, h, w, c).permute(0, 3, 1, 2), None, None, None, *grads)
+
+
+def bits12_ok(ctx):
+    """BN folding needs the fused forward with its relu bits and epilogue statistics (not the BN2 prologue)."""
+    return _FUSE and _LINK and _BITS and not _BN2X
 
 
 def fused_ok(blk, x):
@@ -411,19 +444,18 @@ class _StemFn(torch.autograd.Function):
         do4 = dout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
         dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db)[0]
         if ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
-            dwp = torch.zeros(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)
+            dwp = torch.empty(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)  # beta 0: overwritten
             L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1)
-            dw = conv_ops.stem_pairs_dw(dwp, c, s)
         else:
-            dw8 = torch.zeros(k, r, s, 8, device=x8.device, dtype=torch.float32)
-            L.conv_wgrad(dy4, x8, dw8, 0.0, st, pad)
-            dw = dw8[..., :c].permute(0, 3, 1, 2)                      # [K, C, R, S] view
+            dwp = torch.empty(k, r, s, 8, device=x8.device, dtype=torch.float32)
+            L.conv_wgrad(dy4, x8, dwp, 0.0, st, pad)
         grads = []
         if grad_sink.enabled(w):
-            w.grad.add_(dw.to(w.grad.dtype))
+            L.stem_dw_add(dwp, w.grad, ctx.pairs)  # straight into the flat gradient's [K, R, S, C] memory
             grad_sink.notify(w)
             grads.append(None)
         else:
+            dw = conv_ops.stem_pairs_dw(dwp, c, s) if ctx.pairs else dwp[..., :c].permute(0, 3, 1, 2)
             grads.append(dw.to(w.dtype).contiguous(memory_format=torch.channels_last))
         for p, (a, direct) in ((gamma, (dg, dg_direct)), (beta, (db, db_direct))):
             if direct:

@@ -132,6 +132,9 @@ def stem_pairs(x, w, stride, pad):
     else:
         xp = F.pad(_nhwc(x), (0, 4 - c, pad, wp - wd - pad, pad, pad)).contiguous()   # [N, Hp, Wp, 4]
         xp = xp.view(n, h + 2 * pad, wp // 2, 8)
+    if (w.is_cuda and w.dtype == torch.bfloat16 and w.is_contiguous(memory_format=torch.channels_last)
+            and c <= 4):  # one dtg packing pass (csrc/kernels/stem.hip)
+        return xp, lib().stem_pack_weights(w), (r, s2)
     w4 = F.pad(w.permute(0, 2, 3, 1), (0, 4 - c, 0, 2 * s2 - s)).reshape(k, r * s2 * 8)  # (r, s//2, s%2, c)
     kp = (r * s2 * 8 + 63) // 64 * 64
     return xp, F.pad(w4, (0, kp - r * s2 * 8)).contiguous(), (r, s2)

@@ -47,6 +47,7 @@ class _Linear(torch.autograd.Function):
             y = gemm(x2, True, w, True, bias=bias32, act=act)
         ctx.act = act
         ctx.has_bias = b is not None
+        ctx.bias_param = b if grad_sink.enabled(b) else None
         ctx.bias_dtype = b.dtype if b is not None else None
         ctx.param = w if grad_sink.enabled(w) else None
         ctx.save_for_backward(x2, w, pre if act == "gelu" else (y if act == "relu" else None))
@@ -61,7 +62,12 @@ class _Linear(torch.autograd.Function):
         elif ctx.act == "relu":
             dy = dy * (saved > 0)
         dx = gemm(dy, True, w, False) if ctx.needs_input_grad[0] else None  # [M,K]
-        db = dy.float().sum(0).to(ctx.bias_dtype) if ctx.has_bias else None
+        db = None
+        if ctx.bias_param is not None and dy.shape[1] % 8 == 0:
+            lib().colsum(dy, ctx.bias_param.grad, True, None, 1)  # bias gradient straight into the flat buffer
+            grad_sink.notify(ctx.bias_param)
+        elif ctx.has_bias:
+            db = dy.float().sum(0).to(ctx.bias_dtype)
         p = ctx.param
         if p is not None:
             gemm(dy, False, x2, False, out=p.grad, beta=1.0)  # wgrad straight into the flat buffer

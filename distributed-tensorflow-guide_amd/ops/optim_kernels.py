@@ -61,6 +61,11 @@ def adam(master, grad, m, v, hyper, mirror=None, b1=0.9, b2=0.999, eps=1e-8, wd=
     _cpu_finish(master, mirror, grad, zero_grad)
 
 
+def hyper_tick(hyper):
+    """hyper[1] += 1 on the device (the step counter the fused applies read)."""
+    lib().hyper_tick(hyper)
+
+
 def axpby(acc, g, alpha, beta):
     """acc = alpha * acc + beta * g (window accumulate for DOWNPOUR / ADAG / SDAG)."""
     if acc.is_cuda:

@@ -32,7 +32,10 @@ class _FlatOptimizer:
         overlap.join()  # side-stream weight gradients done before the apply reads them
         self.step_count += 1
         with trace_range("dtg.apply"):  # roctx range (DTG_TRACE=1)
-            self.hyper[1].add_(1.0)
+            if self.hyper.is_cuda:
+                K.hyper_tick(self.hyper)  # dtg kernel (no framework elementwise launch on the step)
+            else:
+                self.hyper[1].add_(1.0)
             for g in self.flat:
                 self._apply(g, grad_scale, zero_grad)
 

@@ -285,3 +285,49 @@ def test_bn_finalize_matches_fwd_part():
     assert torch.allclose(sc, gamma * i2, rtol=1e-6) and torch.allclose(sh, beta - m2 * sc, rtol=1e-5, atol=1e-6)
     assert float(part2.abs().sum()) == 0.0  # the pooled slots go back zeroed
     assert _rel(out, torch.relu(y.float() * sc + sh).to(torch.bfloat16)) < 1e-3
+
+
+@pytest.mark.parametrize("M,Kc,N,accum", [(4096, 256, 64, False), (2048, 64, 256, True), (1024, 512, 128, True),
+                                          (1000, 128, 512, False)])
+def test_bn_folded_dgrad(M, Kc, N, accum):
+    """BN backward folded into the following 1x1 dgrad (batchnorm.hip bn_fold_weights, gemm_bn(a2=, colbias=)):
+    [dp | y] x [diag(a) W ; diag(bx) W] + c^T W, then the mode-3 mask / residual / statistics epilogue, against
+    fp32 torch: dy = a*dp + bx*y + c from bn_bwd_coef, dx = dy W, masked."""
+    L = lib()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(4)
+    dp = torch.randn(M, Kc, generator=g).to(dev, torch.bfloat16)
+    y = (torch.randn(M, Kc, generator=g) * 2 + 0.5).to(dev, torch.bfloat16)
+    W = (torch.randn(Kc, N, generator=g) / Kc ** 0.5).to(dev, torch.bfloat16)
+    # BN statistics of y and the (sum dp, sum dp*xhat) partials in slot 0
+    mean_y = y.float().mean(0)
+    inv_y = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-5)
+    gam = (torch.rand(Kc, generator=g) + 0.5).to(dev)
+    part = torch.zeros(SLOTS, 2, Kc, device=dev)
+    part[0, 0] = dp.float().sum(0)
+    part[0, 1] = (dp.float() * (y.float() - mean_y) * inv_y).sum(0)
+    dgam, dbet = torch.zeros(Kc, device=dev), torch.zeros(Kc, device=dev)
+    coef = L.bn_bwd_coef(part.view(-1), gam, mean_y, inv_y, dgam, dbet, M)
+    a, bx, c = coef.view(3, Kc)
+    dy_ref = a * dp.float() + bx * y.float() + c
+    # the BN the dgrad output feeds (mode 3: its relu mask as bits, its statistics)
+    x = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    mean, inv, gamma, beta = _chan(N, dev, g)
+    mask = (torch.rand(M, N, generator=g) > 0.4).to(dev)
+    bits = (mask.view(M, N // 8, 8).to(torch.uint8) << torch.arange(8, device=dev, dtype=torch.uint8)).sum(-1)
+    bits = bits.to(torch.uint8).contiguous()
+    res = torch.randn(M, N, generator=g).to(dev, torch.bfloat16) if accum else None
+    Wab, cw = L.bn_fold_weights(W, coef)
+    out = res.clone() if accum else None
+    o, part_o = L.gemm_bn(dp, Wab, 3, x, mean, inv, gamma, beta, mask=bits, out=out, a2=y, colbias=cw)
+    torch.cuda.synchronize()
+    ref = dy_ref @ W.float() + (res.float() if accum else 0)
+    ref = torch.where(mask, ref, torch.zeros_like(ref))
+    assert _rel(o, ref) < 1.5e-2, _rel(o, ref)
+    s_ref = ref.sum(0)
+    q_ref = (ref * (x.float() - mean) * inv).sum(0)
+    s, q = _bn_stats(part_o, N)
+    assert _rel(s, s_ref) < 2e-2 and _rel(q, q_ref) < 2e-2
+    # the side-stream half: dy from the same coefficients
+    dy = L.bn_dx_coef(dp, y, coef)
+    assert _rel(dy, dy_ref) < 1e-2

@@ -330,11 +330,15 @@ def test_resnet50_full_network_matches_fp32_reference():
     assert e_bad > 3.0 * _med(e_emu.values()) and e_bad > 0.1
 
 
-def test_bottleneck_chain_matches_fp32_reference():
+@pytest.mark.parametrize("fold", [False, True])
+def test_bottleneck_chain_matches_fp32_reference(fold, monkeypatch):
     """Three fused bottleneck nodes in a row -- a projection block (stride 1), an identity block and a strided
     projection block, linked through the cross-block BN3 reduction -- against F.conv2d / F.batch_norm in fp32
-    with dtg's bf16 storage points emulated: output, input gradient and every parameter gradient."""
+    with dtg's bf16 storage points emulated: output, input gradient and every parameter gradient.  ``fold``:
+    BN1 / BN3 backward folded into the 1x1 dgrads (resnet_fused._FOLD)."""
     from dtg.models.resnet import Bottleneck
+    from dtg.models import resnet_fused
+    monkeypatch.setattr(resnet_fused, "_FOLD", fold)
     torch.manual_seed(0)
     dev = torch.device("cuda")
     chain = torch.nn.Module()
