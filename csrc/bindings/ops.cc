@@ -380,12 +380,8 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad) {
   return y;
 }
 
-// DTG_DGRAD_WT=1: stride-1 dgrad reads the weight transposed to [C][(r,s,k)] (K-contiguous) instead of
-// the MN-contiguous image; measured equal within +-5 % on the ResNet-50 3x3 layers (off by default)
-static bool dgrad_wt() {
-  static const bool on = getenv("DTG_DGRAD_WT") && getenv("DTG_DGRAD_WT")[0] == '1';
-  return on;
-}
+// (a stride-1 dgrad that read the weight transposed to [C][(r,s,k)] measured equal within +-5 % on the
+// ResNet-50 3x3 layers and was retired; conv_dgrad's wT argument stays for the kernel's K-contiguous form)
 
 // dx (= or +=, beta) dgrad; `out` (optional, [N,H,W,C] bf16) receives it in place.  zero_rest=False: a
 // strided dgrad leaves the rows no filter tap reaches unwritten (see gemm_bn's sub2_hw)
@@ -408,7 +404,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     TORCH_CHECK(beta == 0.0, "beta != 0 needs out");
     dx = at::empty({N, H, W, C}, dy.options());
   }
-  Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();  // see conv_dgrad_bn
+  Tensor wT;
   TORCH_CHECK(zero_rest || (stride == 2 && R == 1 && S == 1 && pad == 0 && beta == 0.0),
               "zero_rest=False is for a stride-2 1x1 dgrad (beta 0)");
   dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, (float)beta, cur_stream(),
@@ -694,15 +690,10 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
   auto part = bn_part(x, K, pooled);
-  // DTG_CONV_HALO=1: 3x3 / s1 / p1, 64 -> 64 (ResNet-50 layer 1) through the direct halo-tile conv
-  // (conv_halo.hip): 16 % faster alone (338 vs 400 us at batch 1024 with the statistics), but it holds all of
-  // every CU's LDS while it runs, and the whole training step measured no faster (profiles/r03_conv_l2), so the
-  // implicit GEMM stays the default
-  static const bool halo_on = getenv("DTG_CONV_HALO") && getenv("DTG_CONV_HALO")[0] == '1';
-  if (halo_on && R == 3 && S == 3 && stride == 1 && pad == 1 && dtg::conv3x3_halo_supported(C, K, H, W, 1)) {
-    dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream(), part.data_ptr<float>());
-    return {y, part};
-  }
+  // The direct halo-tile conv for 3x3 / s1 / p1, 64 -> 64 (ResNet-50 layer 1)
+  // (conv_halo.hip, bound as conv_halo_fwd_bn): 16 % faster alone (338 vs 400 us at batch 1024 with the
+  // statistics), but it holds all of every CU's LDS while it runs, and the whole training step measured no
+  // faster (profiles/r03_conv_l2), so the implicit GEMM is the path here
   dtg::BnEpi bn;
   bn.part = part.data_ptr<float>();
   bn.mode = 1;
@@ -737,7 +728,7 @@ std::tuple<Tensor, Tensor> conv_dgrad_bn(Tensor dy, Tensor w, int64_t H, int64_t
     bn.maskbits = mb;
   }
   // stride 1: the kernel reads the weight transposed to [C][(r,s,k)] (K-contiguous; ~1 MB, one small copy)
-  Tensor wT = stride == 1 && dgrad_wt() ? w.permute({3, 1, 2, 0}).contiguous() : Tensor();
+  Tensor wT;
   TORCH_CHECK(dtg::conv_dgrad(cbfp(dy), cbfp(w), bfp(dx), N, H, W, C, K, R, S, stride, pad, 0.f, cur_stream(), bn,
                               wT.defined() ? cbfp(wT) : nullptr),
               "conv_dgrad_bn: geometry leaves rows unwritten (use conv_dgrad + bn_bwd)");
@@ -1077,6 +1068,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("softmax_xent", &softmax_xent);
   m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
+  m.def("gemm_bn_force_cfg", [](int64_t c) { dtg::gemm_bn_force_cfg((int)c); });
   m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });
   m.def("softmax_xent_bwd", &softmax_xent_bwd);
   m.def("gemm_pick_split", [](int64_t M, int64_t N, int64_t K, bool a_kc, int64_t target_wgs) {

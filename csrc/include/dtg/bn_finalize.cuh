@@ -38,19 +38,10 @@ inline BnGeom bn_geom(long long M, int C) {
 // 2 x RPP rows, i.e. every thread streams exactly two rows of its 8 channels (all loads in flight, then the
 // stores) and exits.  Measured against the previous ~2048 long-running workgroups (tools/bn_bench.py,
 // profiles/r03_bn_grid): ResNet-50's largest apply+residual pass 5.0 -> 5.7 TB/s, its dx pass 5.1 -> 6.2
-// TB/s, i.e. the 6.0 TB/s of a plain torch.add moving the same bytes.  DTG_BN_EWG=<workgroups> restores
-// the fixed-count grid for A/B runs.
+// TB/s, i.e. the 6.0 TB/s of a plain torch.add moving the same bytes.
 inline long long elementwise_rpc(const BnGeom& g, long long M) {
-  const int rpp = kBlk / g.tpr;
-  static const long long wgs = getenv("DTG_BN_EWG") ? atoll(getenv("DTG_BN_EWG")) : 0;
-  if (wgs <= 0) return 2LL * rpp;
-  long long nc = wgs / g.gy;
-  const long long max_chunks = (M + rpp - 1) / rpp;
-  if (nc > max_chunks) nc = max_chunks;
-  if (nc < 1) nc = 1;
-  long long rpc = (M + nc - 1) / nc;
-  rpc = (rpc + rpp - 1) / rpp * rpp;  // whole row groups per chunk
-  return rpc;
+  (void)M;
+  return 2LL * (kBlk / g.tpr);
 }
 
 // ---- finalize: reduce chunk partials (double), emit per-channel coefficients -----------------

@@ -152,6 +152,7 @@ struct GemmBatch {
 };
 // force one GEMM tile configuration (sweeps; 0 = heuristic, 99 = 8-phase 256x256)
 void gemm_force_cfg(int cfg);
+void gemm_bn_force_cfg(int cfg);
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
 int gemm_pick_split(int M, int N, int K, int a_kc = 0, int target_wgs = 0);  // target 0: default (512)
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
@@ -270,7 +271,7 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
 void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad
 // stride_w (0 = stride): the W stride where it differs from the H stride (C8 forward and wgrad only)
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w = 0,
-                     int target_wgs = 0);  // target 0: DTG_WGRAD_BLOCKS or 1024
+                     int target_wgs = 0);  // target 0: 1024 workgroups
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
                 int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w = 0);
 

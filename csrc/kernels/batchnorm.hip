@@ -302,19 +302,10 @@ __global__ void __launch_bounds__(kBlk) bn_bwd_dx_kernel(const bf16_t* __restric
   }
 }
 
-static int bn_ru() {  // rows per loop iteration of the streaming passes (2 = one iteration per thread, see
-                     // elementwise_rpc; DTG_BN_RU=4 for A/B runs with DTG_BN_EWG)
-  static const int ru = getenv("DTG_BN_RU") && atoi(getenv("DTG_BN_RU")) == 4 ? 4 : 2;
-  return ru;
-}
-#define DTG_RU_SWITCH(...)                                 \
-  if (bn_ru() == 2) { constexpr int RU = 2; __VA_ARGS__; } \
-  else { constexpr int RU = 4; __VA_ARGS__; }
-
-static bool bn_nt_loads() {
-  static const bool on = !getenv("DTG_BN_NT") || atoi(getenv("DTG_BN_NT")) != 0;
-  return on;
-}
+// RU = 2 rows per loop iteration of the streaming passes: with elementwise_rpc's two rows per thread, one
+// iteration with every load in flight, then the stores
+#define DTG_RU_SWITCH(...) \
+  { constexpr int RU = 2; __VA_ARGS__; }
 
 // ---------------------------------------------------------------------------------------------
 static void bn_apply_launch(const BnGeom& g, const bf16_t* x, const bf16_t* res, bf16_t* y, const float* coef,
@@ -527,10 +518,7 @@ void bn_dx_from_coef(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_
   dim3 ga((unsigned)((M + rpa - 1) / rpa), g.gy);
   const float* ws = coef;
   DTG_TPR_SWITCH(g.tpr, DTG_RU_SWITCH({
-    if (!bn_nt_loads()) {  // DTG_BN_NT=0: plain loads (A/B)
-      if (dres) { bn_bwd_dx_kernel<T, false, true, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
-      else { bn_bwd_dx_kernel<T, false, false, false, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
-    } else if (dres) { bn_bwd_dx_kernel<T, false, true, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C,
+    if (dres) { bn_bwd_dx_kernel<T, false, true, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C,
                                                                                       rpa); DTG_LAUNCH_CHECK(); }
     else { bn_bwd_dx_kernel<T, false, false, true, RU><<<ga, kBlk, 0, st>>>(dp, nullptr, x, ws, dx, dres, M, C, rpa); DTG_LAUNCH_CHECK(); }
   }));
@@ -547,26 +535,45 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
 //   dx[p, n] = sum_k dy[p, k] W[k, n] = sum_k dp[p, k] (a_k W[k, n]) + sum_k x[p, k] (bx_k W[k, n]) + sum_k c_k W[k, n]
 // so the dgrad is ONE GEMM over the K-concatenation [dp | x] with the weights [diag(a) W ; diag(bx) W] (rounded to
 // bf16 once here) plus the constant row cw = c^T W (fp32, added in the epilogue) -- no dx pass over HBM.
-// W [K][N] (row stride ldw); Wab [2K][N] contiguous.  One thread per column n, rows in order: coalesced rows,
-// deterministic column sums.
+// W [K][N] (row stride ldw); Wab [2K][N] contiguous.  Block = 64 columns x 4 row slices (one wave each): lanes
+// take consecutive columns (coalesced rows), each wave a quarter of the rows, 8 rows of loads in flight; the
+// four slices' partial cw meet in LDS in slice order (deterministic).
 __global__ void __launch_bounds__(256) bn_fold_weights_kernel(const bf16_t* __restrict__ W, long long ldw,
                                                               const float* __restrict__ coef, bf16_t* __restrict__ Wab,
                                                               float* __restrict__ cw, int K, int N) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int k0 = (int)((long long)K * sl / 4), k1 = (int)((long long)K * (sl + 1) / 4);
   float s = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float w = bf2f(W[(long long)k * ldw + n]);
-    Wab[(long long)k * N + n] = f2bf(coef[k] * w);
-    Wab[(long long)(K + k) * N + n] = f2bf(coef[K + k] * w);
-    s = fmaf(coef[2 * K + k], w, s);
+  if (n < N) {
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = bf2f(W[(long long)(k + u) * ldw + n]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        Wab[(long long)(k + u) * N + n] = f2bf(coef[k + u] * w[u]);
+        Wab[(long long)(K + k + u) * N + n] = f2bf(coef[K + k + u] * w[u]);
+        s = fmaf(coef[2 * K + k + u], w[u], s);
+      }
+    }
+    for (; k < k1; ++k) {
+      const float w = bf2f(W[(long long)k * ldw + n]);
+      Wab[(long long)k * N + n] = f2bf(coef[k] * w);
+      Wab[(long long)(K + k) * N + n] = f2bf(coef[K + k] * w);
+      s = fmaf(coef[2 * K + k], w, s);
+    }
   }
-  cw[n] = s;
+  part[sl][lane] = s;
+  __syncthreads();
+  if (sl == 0 && n < N) cw[n] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
                      hipStream_t st) {
-  bn_fold_weights_kernel<<<(N + 255) / 256, 256, 0, st>>>(W, ldw, coef, Wab, cw, K, N); DTG_LAUNCH_CHECK();
+  bn_fold_weights_kernel<<<(N + 63) / 64, 256, 0, st>>>(W, ldw, coef, Wab, cw, K, N); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

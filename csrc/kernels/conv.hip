@@ -435,15 +435,11 @@ static bool conv_skinny(int n) { return n <= 64; }
 
 // LDS ring depth of the implicit-GEMM kernels: 1 (32-40 KB of LDS, ~4 workgroups per CU hide latency
 // across blocks) or 2 (64-80 KB, 2 per CU, DMA of the next K-step under the current one).
-// DTG_CONV_STAGES / conv_set_stages() select it per pass (fwd, dgrad, wgrad) for A/B runs.
+// conv_set_stages() overrides it per pass (fwd, dgrad, wgrad) for A/B tools (tools/conv_sweep.sh).
 // Default (measured, profiles/r01_tiles): one stage, except fwd/dgrad grids shorter than 512
 // 128x128 tiles with a reduction of >= 2048 (the 7x7 / 512-channel layers), which keep the 2-deep ring.
-static int g_conv_stages[3] = {0, 0, 0};
+static int g_conv_stages[3] = {-1, -1, -1};
 static int conv_stages(int which, long long M = 0, int N = 0, int Kred = 0) {
-  if (g_conv_stages[which] == 0) {
-    const char* f = getenv("DTG_CONV_STAGES");
-    g_conv_stages[which] = f ? (atoi(f) >= 1 && atoi(f) <= 3 ? atoi(f) : 2) : -1;
-  }
   if (g_conv_stages[which] > 0) return g_conv_stages[which];
   if (which == 2) return 1;
   const long long tiles = ((M + 127) / 128) * ((N + 127) / 128);
@@ -460,6 +456,7 @@ static void run_sched(int sched, F&& run) {
   else if (sched == 2) run(Cfg<BM, BN, 2>());
   else run(Cfg<BM, BN, 1, 4, 64, true>());
 }
+
 
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which) {
   if (C == 8 && K % 64 == 0 && which != 1) return 1;  // stem: fwd (conv_fwd_c8) and wgrad
@@ -601,11 +598,9 @@ int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   const long long tiles = K <= 64 ? (long long)((No + 255) / 256) : (long long)((K + 127) / 128) * ((No + 127) / 128);
-  // target workgroups (DTG_WGRAD_BLOCKS, default 1024 = 4 single-stage workgroups per CU; measured 3-5 %
-  // faster than 512 on the 14x14 / 28x28 3x3 layers, 256 is 25 % slower); more splits also grow the fp32
-  // slabs the reduce pass re-reads
-  static const long long dflt = getenv("DTG_WGRAD_BLOCKS") ? atoll(getenv("DTG_WGRAD_BLOCKS")) : 1024;
-  const long long target = target_wgs > 0 ? target_wgs : dflt;
+  // target workgroups (default 1024 = 4 single-stage workgroups per CU; measured 3-5 % faster than 512 on the
+  // 14x14 / 28x28 3x3 layers, 256 is 25 % slower); more splits also grow the fp32 slabs the reduce pass re-reads
+  const long long target = target_wgs > 0 ? target_wgs : 1024;
   // up to 1024 splits when the fp32 slabs stay small (<= 64 MB): the stem's single 64 x 224 output tile
   // needs 1024 splits to reach 1024 workgroups (at 256 it ran 256 workgroups, one per CU)
   const long long slab = (long long)K * No * 4;

@@ -306,12 +306,10 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
 
 }  // namespace
 
-// DTG_HALO_MODE: 0 (default) persistent + double-buffered halo, weights resident in LDS; 1 one band per
-// workgroup with the weights read from global; 2 one band per workgroup with the weights staged in LDS too
-static int halo_mode() {
-  static const int m = getenv("DTG_HALO_MODE") ? atoi(getenv("DTG_HALO_MODE")) : 0;
-  return m;
-}
+// Schedule: 0 persistent + double-buffered halo, weights resident in LDS (the only one built into the
+// launcher); the per-band modes 1 (weights from global) and 2 (weights staged per band) stay compiled for
+// tools/conv_halo_ab.py history but are not selectable any more (both measured slower, profiles/r03_*halo*)
+static int halo_mode() { return 0; }
 
 static size_t conv3x3_halo_lds(int W, int mode) {
   const size_t halo = (size_t)(kTH + 2) * (W + 2) * 128, wts = 9 * 64 * 128, stage = 4 * 64 * 128;

@@ -92,19 +92,10 @@ long long gemm_workspace_floats(int M, int N, int K, int split_k) {
 
 static bool skinny(int N) { return N <= 64; }
 
-// DTG_WGRAD8=1 (experiment): weight gradients (both operands MN-contiguous, M and N multiples of 256) on the
-// 256x256 8-wave kernel (gemm8.hip), split-K sized for its tiles
-static bool wgrad8() {
-  static const bool on = getenv("DTG_WGRAD8") && getenv("DTG_WGRAD8")[0] == '1';
-  return on;
-}
-static bool wgrad8_shape(int M, int N, int a_kc) { return wgrad8() && !a_kc && M % 256 == 0 && N % 256 == 0; }
-
 static bool short_m(int M, int N) { return M <= 64 && N >= 128; }
 
 int gemm_pick_split(int M, int N, int K, int a_kc, int target_wgs) {
-  int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
-  if (wgrad8_shape(M, N, a_kc)) BMv = BNv = 256;
+  const int BMv = skinny(N) ? 256 : (short_m(M, N) ? 64 : 128), BNv = skinny(N) ? 64 : (short_m(M, N) ? 256 : 128);
   const long long tiles = (long long)((M + BMv - 1) / BMv) * ((N + BNv - 1) / BNv);
   // forward / data-gradient GEMMs (K-contiguous A) with >= 128 tiles: the fp32 partial round trip
   // costs more than the idle CUs do (BERT 8192x768x3072: 47 us unsplit, 56 us split 2;
@@ -119,10 +110,8 @@ int gemm_pick_split(int M, int N, int K, int a_kc, int target_wgs) {
     return s;
   }
   int s = 1;
-  // aim for >= ~512 workgroups while keeping >= 1024 K (16 K-steps) per split (DTG_GEMM_SPLIT_WGS
-  // overrides the workgroup target for A/B runs)
-  static const long long dflt = getenv("DTG_GEMM_SPLIT_WGS") ? atoll(getenv("DTG_GEMM_SPLIT_WGS")) : 512;
-  const long long target = target_wgs > 0 ? target_wgs : dflt;
+  // aim for >= ~512 workgroups (or the caller's target) while keeping >= 1024 K (16 K-steps) per split
+  const long long target = target_wgs > 0 ? target_wgs : 512;
   while (tiles * s < target && (long long)K / (s * 2) >= 1024 && s < 256) s *= 2;
   return s;
 }
@@ -144,66 +133,20 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   }
 }
 
-// 256x256 / 8-wave / 8-phase kernel (gemm8.hip) for GEMMs big enough to fill the chip with 256x256
-// tiles.  Opt-in (DTG_GEMM8=1 forces it on, DTG_GEMM8=2 applies the heuristic below): on the only
-// shapes of the flagship steps that reach it, BERT's MLM decoder GEMMs, it lost to the 128x128
-// single-stage kernels (30528x768x5120 wgrad 419 vs 289 us; 5120x768x30528 dgrad 834 vs 286 us split 2;
-// profiles/r02_gemm).
-static bool use_8phase(int M, int N, int K, int split_k) {
-  const char* f = getenv("DTG_GEMM8");
-  if (!f || f[0] == '0') return false;
-  if (f[0] == '1') return M >= 256 && N >= 128;
-  // Both kernels run one "round" of tiles at a time (256x256: 1 workgroup per CU; 128x128: 2 per
-  // CU), so compare round utilisation, crediting the 8-phase kernel with its per-CU advantage, which
-  // grows with K (measured, profiles/r01_gemm8: ~1.15x at K = 768 in a cold-cache training step, up
-  // to ~2x at K >= 2048); it loses at K = 256 (prologue/epilogue dominated).
-  // r01_tiles sweep: at K <= 3072 the single-stage 128x128 / 64x256 rings match or beat it
-  if (split_k != 1 || M < 256 || N < 256 || K < 4096) return false;
-  const long long t8 = (long long)((M + 255) / 256) * ((N + 255) / 256);
-  const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
-  if (t8 < 48) return false;
-  const double u8 = (double)t8 / (double)(((t8 + 255) / 256) * 256);
-  const double u128 = (double)t128 / (double)(((t128 + 511) / 512) * 512);
-  const double gain = K >= 2048 ? 2.1 : (K >= 1024 ? 1.4 : 1.15);
-  return u8 * gain > u128;
-}
-
-// 256x128 tile, 8 waves, one workgroup per CU, 3-slot LDS ring with counted vmcnt (prefetch
-// distance 2).  Chosen when the grid still fills the chip with these larger tiles and K per block
-// is long enough for the deeper pipeline to matter.
-static bool use_big(int M, int N, int kps, int split_k, const GemmBatch& bt) {
-  if (const char* f = getenv("DTG_GEMM_BIG")) return f[0] == '1';
-  return false;  // measured slower than the 2-block 128x128 ring on every shape (profiles/r01_gemm_ab); opt-in only
-  const long long tiles = (long long)((M + 255) / 256) * ((N + 127) / 128) * split_k * bt.count;
-  return N >= 128 && tiles >= 192 && kps >= 4 * BK;
-}
-
-static void launch_big(int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M,
-                       int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
-                       const GemmBatch& bt) {
-  using CF = Cfg<256, 128, 3, 8>;
-  const bool full = (M % 256 == 0) && (N % 128 == 0) && (K % BK == 0);
-  if (full) launch_layout<CF, false>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-  else launch_layout<CF, true>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-}
-
+// (The 256x256 8-wave 8-phase kernel, gemm8.hip, lost to the 128x128 single-stage kernels on every flagship
+// shape -- BERT's MLM decoder 30528x768x5120 wgrad 419 vs 289 us, 5120x768x30528 dgrad 834 vs 286 us split 2,
+// profiles/r02_gemm -- and the 256x128 8-wave 3-slot ring on every shape of profiles/r01_gemm_ab: both are
+// reachable only through the forced-configuration table, gemm_force_cfg, for the A/B tools.)
 
 // forced tile configurations (tools/gemm_sweep.py): gemm_forced.hip
 bool gemm_launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb,
                         int M, int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
                         const GemmBatch& bt);
-// DTG_GEMM_RP=0 turns off the register-pipelined single-stage tile (A/B switch)
-static bool gemm_rp() {
-  static const bool on = !(getenv("DTG_GEMM_RP") && getenv("DTG_GEMM_RP")[0] == '0');
-  return on;
-}
-
 // Register pipelining pays when each workgroup has a long K loop and the problem is compute-heavy
 // enough that latency, not occupancy (3 instead of 4 workgroups per CU), limits it: long K (>= 2048),
 // or K >= 768 at >= 300 flop per operand byte (BERT's 8192-token GEMMs: 5-12 % faster; ResNet's
 // 50176x256x1024 at 204 flop/B is 8 % slower with it).
 static bool use_rp(int M, int N, int kps) {
-  if (!gemm_rp()) return false;
   // ... but only while the grid is short: with more than ~2 rounds of 128x128 tiles (> 2048 at 4 per CU)
   // the fourth resident workgroup the plain single stage keeps is worth more than in-block pipelining
   // (BERT-base at 32768 tokens: 32768x3072x768 990 vs 896 TF/s, 32768x2304x768 979 vs 922; at
@@ -214,14 +157,9 @@ static bool use_rp(int M, int N, int kps) {
   return kps >= 768 && flop / bytes >= 300.0;
 }
 
-static int g_forced_cfg = -1;
-static int forced_cfg() {
-  if (g_forced_cfg < 0) {
-    const char* f = getenv("DTG_GEMM_CFG");
-    g_forced_cfg = f ? atoi(f) : 0;
-  }
-  return g_forced_cfg;
-}
+// forced tile configuration for the A/B tools (tools/gemm_ab.py, gemm_sweep.py): 0 = the heuristics below
+static int g_forced_cfg = 0;
+static int forced_cfg() { return g_forced_cfg; }
 void gemm_force_cfg(int cfg) { g_forced_cfg = cfg; }
 
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
@@ -253,39 +191,25 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
     }
     if (gemm_launch_forced(fc, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt)) return;
   }
-  if (bt.count == 1 && use_8phase(M, N, K, split_k)) {
-    gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
-    return;
-  }
-  if (bt.count == 1 && !b_kc && wgrad8_shape(M, N, a_kc)) {
-    gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
-    return;
-  }
   if (split_k > 1 || !a_kc) {
     // weight gradients (MN-contiguous A, split-K over the token/pixel dimension): the single-stage
     // 128x128 ring beat every other tile and the 2-stage ring on all of them, BERT's 768x3072x8192
     // by 1.4x (profiles/r01_tiles/sweep_wgrad.json); its register-pipelined variant (next K-step's DMA
     // issued under this step's MFMAs) is another 5-8 % on all wgrad shapes but one (sweep_rp.json)
-    if (gemm_rp()) launch_exact<Cfg<128, 128, 1, 4, 64, true>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-    else launch_exact<Cfg<128, 128, 1>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
+    // (round 4, measured in the ResNet-50 b1024 step and alone at 128 workgroups, tools/gemm_ab.py --layout tn,
+    // profiles/r04_wgrad: a 2-4 slot LDS-DMA ring 6-18 % slower alone and 4-9 % slower in the step; the
+    // 256x128 8-wave tile 28 % faster alone at equal workgroups but neutral in the step; 256x256 gemm8 tiles
+    // -0.5 %: the side-stream weight gradients cost the step HBM bandwidth, not CU time)
+    launch_exact<Cfg<128, 128, 1, 4, 64, true>>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
     return;
   }
   if (short_m(M, N)) {  // 64-row outputs: no half-empty 128-row tiles
     launch_cfg<64, 256>(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
     return;
   }
-  if (use_big(M, N, kps, split_k, bt)) {
-    launch_big(a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt);
-    return;
-  }
-  // opt-in (DTG_GEMM_WIDE=1): wide outputs over a short reduction (BERT's FFN1 forward / FFN2 dgrad,
-  // 32768x3072x768) on the 128x256 8-wave single stage.  Plain GEMMs measured 156 vs 165 us (nt) and 163
-  // vs 167 us (nn) in tools/gemm_ab.py (profiles/r02_gemm/gemm_ab_8wave_*.txt), but with the real GELU /
-  // aux epilogues BERT-base b256 ran 8.92k vs 9.05k seq/s (profiles/r02_gemm/bert_wide*.log): off.
-  static const bool wide_on = getenv("DTG_GEMM_WIDE") && atoi(getenv("DTG_GEMM_WIDE")) != 0;
-  if (wide_on && split_k == 1 && bt.count == 1 && N >= 3072 && kps <= 1024 && M >= 8192 &&
-      gemm_launch_forced(29, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt))
-    return;
+  // (the 128x256 8-wave single stage for wide outputs over a short reduction -- BERT's FFN1 forward / FFN2
+  // dgrad -- won 156 vs 165 us as a plain GEMM but lost with the real GELU / aux epilogues, 8.92k vs 9.05k
+  // seq/s, profiles/r02_gemm: forced configuration 29 only)
   // Tile width follows N so the streamed activation operand A is read as few times as possible:
   // 256x64 for N <= 64, 64x256 for N >= 256 with K <= 256, else 128x128 (r01_tiles sweeps).  LDS ring depth: a single stage
   // (32-40 KB: ~4 workgroups per CU hide the HBM latency across blocks) unless the grid is short
@@ -327,8 +251,6 @@ static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long
                      dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn); DTG_LAUNCH_CHECK();
 }
 
-// DTG_BN_PF: 0 never prefetch, 2 always, default 1 = the shape rule in launch_bn_cfg
-static const int g_bn_pf = getenv("DTG_BN_PF") ? atoi(getenv("DTG_BN_PF")) : 1;
 
 template <class CF, int MODE>
 static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
@@ -337,7 +259,7 @@ static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long 
   // prefetching backward epilogue where the epilogue's streaming dominates: wide outputs or short
   // reductions (measured per shape, profiles/r02_epi_pf; see epilogue_bn)
   if constexpr (MODE >= 2 && MODE <= 4) {
-    if (g_bn_pf != 0 && (g_bn_pf == 2 || N >= 512 || K <= 128)) {
+    if (N >= 512 || K <= 128) {
       if (full) launch_bn<CF, MODE, false, true>(A, lda, B, ldb, M, N, K, e, bn, st);
       else launch_bn<CF, MODE, true, true>(A, lda, B, ldb, M, N, K, e, bn, st);
       return;
@@ -347,9 +269,10 @@ static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long 
   else launch_bn<CF, MODE, true, false>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
-// DTG_BN_GEMM_CFG forces the BN-epilogue GEMM tile (A/B runs): 1 128x128, 2 64x256, 3 128x128 register-
-// pipelined, 4 256x64, 5 128x256 8 waves, 6 256x128 8 waves; 0 = the heuristic below
-static const int g_bn_gemm_cfg = getenv("DTG_BN_GEMM_CFG") ? atoi(getenv("DTG_BN_GEMM_CFG")) : 0;
+// gemm_bn_force_cfg (tools/bn_gemm_ab.py) forces the BN-epilogue GEMM tile: 1 128x128, 2 64x256, 3 128x128
+// register-pipelined, 4 256x64, 5 128x256 8 waves, 6 256x128 8 waves; 0 = the heuristic below
+static int g_bn_gemm_cfg = 0;
+void gemm_bn_force_cfg(int cfg) { g_bn_gemm_cfg = cfg; }
 
 template <int MODE>
 static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
@@ -443,9 +366,8 @@ void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
   BnEpi bn;
   bn.xcoef = coef;
   bn.xc_n = N;
-  // the weight-gradient tile of gemm_bf16 (single-stage 128x128, register-pipelined unless DTG_GEMM_RP=0)
-  if (gemm_rp()) launch_xb_cfg<Cfg<128, 128, 1, 4, 64, true>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
-  else launch_xb_cfg<Cfg<128, 128, 1>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
+  // the weight-gradient tile of gemm_bf16 (single-stage 128x128, register-pipelined)
+  launch_xb_cfg<Cfg<128, 128, 1, 4, 64, true>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
 }
 
 void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,

@@ -1,4 +1,4 @@
-// Forced GEMM tile configurations (DTG_GEMM_CFG / gemm_force_cfg): the table tools/gemm_sweep.py and
+// Forced GEMM tile configurations (gemm_force_cfg): the table tools/gemm_sweep.py and
 // tools/gemm_ab.py measure the heuristic in gemm.hip against.  Split over three translation units
 // (gemm_forced*.hip) so the instantiations compile in parallel.
 #include "dtg/gemm_launch.cuh"

@@ -394,8 +394,7 @@ static size_t stem_band_lds(int Q, int C) {
 }
 
 static bool stem_band_ok(int H, int C, int k, int s, int pad, int P, int Q) {
-  static const bool on = !getenv("DTG_STEM_BAND") || atoi(getenv("DTG_STEM_BAND")) != 0;
-  return on && k == 3 && s == 2 && pad == 1 && C == 64 && H % kStemBandRows == 0 && P == (H - 1) / 2 + 1 &&
+  return k == 3 && s == 2 && pad == 1 && C == 64 && H % kStemBandRows == 0 && P == (H - 1) / 2 + 1 &&
          stem_band_lds(Q, C) <= (size_t)160 * 1024;
 }
 
@@ -473,9 +472,8 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                                                          sinv, momentum, eps, coef, nullptr, nullptr, 0); DTG_LAUNCH_CHECK();
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   const long long total = (long long)N * P * Q * (C / 8);
-  // 3x3 windows (ResNet): the unrolled form with raw-vector loads (DTG_STEM_POOL_KT=0: the runtime loop)
-  static const bool kt3 = !getenv("DTG_STEM_POOL_KT") || atoi(getenv("DTG_STEM_POOL_KT")) != 0;
-  if (k == 3 && kt3)
+  // 3x3 windows (ResNet): the unrolled form with raw-vector loads; other windows: the runtime loop
+  if (k == 3)
     hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
   else
     hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);

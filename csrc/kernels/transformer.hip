@@ -523,16 +523,8 @@ void ln_fwd(const bf16_t* h, const bf16_t* res, const float* gamma, const float*
 }
 
 // Blocks of the LayerNorm backward (each folds its rows' dgamma/dbeta/dbias into one partial row of
-// the workspace).  DTG_LN_BWD_BLOCKS overrides the cap (A/B runs).
-static int ln_bwd_cap() {
-  static int cap = -1;
-  if (cap < 0) {
-    const char* v = getenv("DTG_LN_BWD_BLOCKS");
-    cap = v ? atoi(v) : 1024;  // 4 blocks (16 waves) per CU: BERT-base b256 8.84k -> 8.88k seq/s over 512
-    if (cap < 64) cap = 1024;
-  }
-  return cap;
-}
+// the workspace): at most 1024 = 4 blocks (16 waves) per CU, BERT-base b256 8.84k -> 8.88k seq/s over 512
+static int ln_bwd_cap() { return 1024; }
 
 int ln_bwd_blocks(int T) {
   const int b = (T + kRowsPerBlock - 1) / kRowsPerBlock, cap = ln_bwd_cap();

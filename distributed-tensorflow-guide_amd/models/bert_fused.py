@@ -20,7 +20,6 @@ embedding's flat gradient without notifying; the embedding node (which runs last
 adds the lookup gradient and notifies once, so the all-reduce bucket holding the embedding sees
 exactly one "ready" event per step.
 """
-import os
 
 import torch
 
@@ -30,7 +29,7 @@ from ..ops import transformer as T
 from ..parallel import grad_sink, overlap
 
 
-_ATTN = os.environ.get("DTG_ATTN", "fused")  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax)
+_ATTN = "fused"  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax; A/B tests)
 
 
 def _fused_attn(S, backward=True):

@@ -18,8 +18,8 @@ projection's accumulates (beta = 1) straight into the conv1 dgrad output.
 BN statistics are fused into the producing GEMM/conv epilogue (csrc/include/dtg/bn_epi.cuh):
 forward, every conv output's per-channel sum / sum of squares; backward, the dgrads feeding BN2 and
 BN1 emit the relu-masked gradient plus sum(dp) and sum(dp*xhat).  Each BN then costs finalize +
-one elementwise pass instead of a reduction pass + finalize + elementwise pass.  DTG_BN_FUSE=0
-restores the separate statistics kernels (A/B runs).
+one elementwise pass instead of a reduction pass + finalize + elementwise pass.  _FUSE = False
+restores the separate statistics kernels (A/B tests).
 
 BN3 of block i (relu(bn3(y3) + identity) = the block output = block i+1's input) is reduced one
 block LATER: block i+1's last dgrad GEMM, the final writer of dL/d out_i, applies block i's relu
@@ -56,22 +56,25 @@ def _krsc(w):  # channels_last [K, C, R, S] -> contiguous [K, R, S, C] view
     return w.permute(0, 2, 3, 1)
 
 
-_FUSE = os.environ.get("DTG_BN_FUSE", "1") != "0"
-_LINK = os.environ.get("DTG_BN3_LINK", "1") != "0"  # cross-block BN3 reduction (needs _FUSE)
+_FUSE = True  # BN statistics in the GEMM/conv epilogues (False: separate statistics kernels, for A/B tests)
+_LINK = True  # cross-block BN3 reduction (needs _FUSE)
 # linked stride-2 projection: its dgrad writes only the even (h, w) rows, which the next mode-3 GEMM alone
 # reads (no zero-fill of a [N, H, W, C] gradient per stage transition); 0 restores the zero-filled form
-_SUB2 = os.environ.get("DTG_DGRAD_SUB2", "1") != "0"
-# DTG_BN2_FUSE=1: BN2 (+ relu) applied in conv3's operand prologues instead of a separate apply pass (needs
+_SUB2 = True
+# _BN2X = True: BN2 (+ relu) applied in conv3's operand prologues instead of a separate apply pass (needs
 # _FUSE): the forward GEMM reads y2 and the BN2 coefficients (gemm_bn xcoef), the weight gradient likewise
 # (gemm_xb); a2 and BN2's relu-mask bits are never written.  Off by default: measured slower, ResNet-50 b512
 # 14.46k vs 14.80k img/s -- the prologue costs the forward GEMMs +0.39 ms and the weight gradients +1.2 ms
 # per step against the 0.55 ms apply pass it removes (profiles/r03_bn2_prologue).
-_BN2X = os.environ.get("DTG_BN2_FUSE", "0") == "1"
-# DTG_BN_FOLD=1: BN3 (identity blocks) and BN1 backward folded into the following 1x1 dgrad -- the dgrad GEMM
-# reads [dp | y] along K against [diag(a) W ; diag(bx) W] plus the constant row c^T W (dy = a*dp + bx*y + c), so the
-# main stream makes no dx pass for them; the weight gradient, which needs dy itself, gets it from a dx pass on the
-# side stream (batchnorm.hip bn_fold_weights, gemm_bn(a2=..., colbias=...)).  Needs _FUSE and _LINK.
-_FOLD = os.environ.get("DTG_BN_FOLD", "0") == "1"
+_BN2X = False
+# _FOLD = True (round-4 experiment, off): BN3 (identity blocks) and BN1 backward folded into the following 1x1
+# dgrad -- the dgrad GEMM reads [dp | y] along K against [diag(a) W ; diag(bx) W] plus the constant row c^T W
+# (dy = a*dp + bx*y + c), so the main stream makes no dx pass for them; the weight gradient, which needs dy itself,
+# gets it from a dx pass on the side stream (batchnorm.hip bn_fold_weights, gemm_bn(a2=..., colbias=...)).
+# Measured 14.2k vs 15.2k img/s at b1024 (profiles/r04_bn_fold): the main stream shortened by 2.3 ms, but the
+# doubled-K dgrads took +3.4 ms and the side stream's dx passes (16 ms there) made it the critical path.  What
+# would remove them is a weight gradient reading [dp | y] with two accumulators (a_k G1 + bx_k G2 + c_k colsum x).
+_FOLD = False
 
 
 class _Bn3Link:
@@ -94,9 +97,9 @@ def _gacc(p):
     return torch.zeros_like(p, dtype=torch.float32 if p.dim() <= 1 else p.dtype), False
 
 
-# DTG_BN_BITS=0: the backward recomputes BN1/BN2's relu masks from y and the BN statistics (mode 2)
+# _BITS = False: the backward recomputes BN1/BN2's relu masks from y and the BN statistics (mode 2)
 # instead of reading the packed masks the forward apply wrote (mode 3, 1/16 of y's bytes)
-_BITS = os.environ.get("DTG_BN_BITS", "1") != "0"
+_BITS = True
 
 
 # Split-K targets (workgroups) of the weight gradients when they run on the side stream (parallel/overlap.py,
@@ -402,8 +405,8 @@ def bottleneck(blk, x):
 # csrc/kernels/stem.hip: the BN statistics come from the conv epilogue, BN+ReLU+pool is one pass over the
 # conv output, and the backward recomputes the pre-pool gradient inside both BN-backward passes, so
 # neither the BN output nor the pre-pool gradient (411 MB each at batch 256) is ever written.
-# DTG_STEM_FUSE=0 restores conv -> BN -> max-pool as separate ops (A/B runs).
-_STEM = os.environ.get("DTG_STEM_FUSE", "1") != "0"
+# _STEM = False restores conv -> BN -> max-pool as separate ops (A/B tests).
+_STEM = True
 _POOL = (3, 2, 1)  # ResNet's stem max-pool: 3x3, stride 2, pad 1
 
 

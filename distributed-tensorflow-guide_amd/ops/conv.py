@@ -1,6 +1,6 @@
 """2-D convolution on NHWC (channels_last) bf16 activations -- dtg's own MFMA kernels.
 
-Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
+Dispatch (module attribute ``_IMPL = "miopen"`` forces the library path for A/B runs):
   * 1x1 / stride 1 / pad 0 -> the MFMA GEMM (csrc/kernels/gemm.hip) on the [N*H*W, C] row view:
         fwd  Y  = X  W^T      dgrad dX = dY W      wgrad dW = dY^T X
   * k x k, C % 64 == 0, K % 64 == 0 -> implicit-GEMM conv (csrc/kernels/conv.hip):
@@ -17,7 +17,6 @@ Dispatch (``DTG_CONV_IMPL=miopen`` forces the library path for A/B runs):
   * everything else -> MIOpen through torch
 Weight gradients are accumulated straight into the flat gradient buffer (see parallel/grad_sink).
 """
-import os
 
 import torch
 import torch.nn.functional as F
@@ -26,7 +25,8 @@ from ..parallel import grad_sink
 from ._native import lib
 from .gemm import gemm
 
-_IMPL = os.environ.get("DTG_CONV_IMPL", "dtg")
+_IMPL = "dtg"
+_PAIRS = True  # the pixel-pair stem conv (stem_pairs); False: the 8-channel padded form
 
 
 def _rows(t):
@@ -141,7 +141,7 @@ def stem_pairs(x, w, stride, pad):
 
 
 def stem_pairs_ok(x, w, stride):
-    return x.shape[1] <= 4 and stride == 2 and os.environ.get("DTG_STEM_PAIRS", "1") != "0"
+    return x.shape[1] <= 4 and stride == 2 and _PAIRS
 
 
 def stem_pairs_dw(dwp, c, s):

@@ -61,10 +61,9 @@ def init(backend=None, timeout_s=None, watchdog=True):
             kw["device_id"] = device
             # collectives on a high-priority stream: its own hardware queue, apart from the main and the
             # (high-priority) wgrad side stream's (parallel/overlap.py; 12.3k -> 14.5k img/s one-rank RCCL)
-            if os.environ.get("DTG_PG_HIPRIO", "1") == "1":
-                opts = dist.ProcessGroupNCCL.Options()
-                opts.is_high_priority_stream = True
-                kw["pg_options"] = opts
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            kw["pg_options"] = opts
         if timeout_s is None:
             timeout_s = float(os.environ.get("DTG_COLLECTIVE_TIMEOUT", "600"))
         dist.init_process_group(backend, rank=rank, world_size=world,

@@ -26,7 +26,6 @@ import torch.distributed as dist
 from . import grad_sink, overlap
 from ..utils.trace import trace_range
 
-_LAUNCH = os.environ.get("DTG_DDP_LAUNCH", "side")  # stream a bucket's collective is enqueued from
 
 
 def _parse_emulate(spec):
@@ -67,7 +66,6 @@ class DataParallel:
         self.overlap = overlap and (self.world > 1 or forced)
         self._force = forced
         self._comm = True  # set_comm(False): gradients stay rank-local (bench.py's compute-only timing)
-        self._cstreams = {}
         self._estreams = {}
         self.emulate = EMULATE if self.overlap else None
         self.buckets = []
@@ -117,12 +115,10 @@ class DataParallel:
                 # hardware queues a HIP process gets by default (GPU_MAX_HW_QUEUES=4), where a separate
                 # launch stream made two streams share a queue and serialise (profiles/r03_streams).  The
                 # side stream's later wgrads need the main stream's later dgrads anyway, so the wait costs
-                # it nothing.  DTG_DDP_LAUNCH=comm restores the third stream (A/B).
+                # it nothing.
                 main = torch.cuda.current_stream(v.device)
-                ls = self._comm_stream(v.device) if _LAUNCH == "comm" else side
+                ls = side
                 ls.wait_stream(main)
-                if ls is not side:
-                    ls.wait_stream(side)
                 with torch.cuda.stream(ls):
                     b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
                 self._emulate(v, ls)
@@ -156,12 +152,6 @@ class DataParallel:
         es.wait_stream(after)
         with torch.cuda.stream(es):
             lib().comm_spin(secs, e["wgs"], 0)
-
-    def _comm_stream(self, device):
-        cs = self._cstreams.get(device.index)
-        if cs is None:
-            cs = self._cstreams[device.index] = torch.cuda.Stream(device=device)
-        return cs
 
     def _on_direct(self, p):
         if p in self._param_bucket:

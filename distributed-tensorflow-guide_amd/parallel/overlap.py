@@ -39,7 +39,7 @@ gloo (host-staged) keeps the wgrads on the main stream: there the side stream ra
 (profiles/r02_overlap), because the staging copies synchronise the host.
 
 ``DTG_WGRAD_STREAM=0`` runs every wgrad on the main stream (A/B runs).  ``=2`` forces the side stream
-with several gloo ranks too.  ``DTG_SIDE_PRIO=0`` gives the side stream normal priority.  Measured gain on one rank:
+with several gloo ranks too.  Measured gain on one rank:
 ResNet-50 +2.3 % (+4 % with the side-stream split targets of models/resnet_fused.py), BERT-base +1.1 %.
 The record_stream version once ran a whole bench 5x slower (191 ms/step instead of 37 ms, same losses),
 most likely because its allocator reserve kept growing (profiles/r02_overlap).
@@ -51,7 +51,7 @@ import torch
 
 _ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
 _MULTI = os.environ.get("DTG_WGRAD_STREAM") == "2"  # also with several ranks (rehearsals)
-_PRIO = int(os.environ.get("DTG_SIDE_PRIO", "-1"))  # torch stream priority of the side stream (-1: high)
+_PRIO = -1  # torch stream priority of the side stream: high (its own hardware queue, see above)
 _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()

@@ -5,6 +5,7 @@ import torch.nn.functional as F
 
 import dtg  # noqa: F401
 from dtg import ops
+from dtg.ops import conv as conv_ops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -93,7 +94,7 @@ def test_conv_dgrad_strided_accumulate(R, st, pad, H):
 def test_conv_c8_stem(N, C, K, H, R, st, pad, pairs, monkeypatch):
     """Few-channel input (the ResNet stem): implicit-GEMM fwd + wgrad on the input padded to 8 channels,
     or (stride 2, <= 4 channels, pairs=1) packed as pixel pairs (ops/conv.py stem_pairs)."""
-    monkeypatch.setenv("DTG_STEM_PAIRS", pairs)
+    monkeypatch.setattr(conv_ops, "_PAIRS", pairs != "0")
     g = torch.Generator(device="cpu").manual_seed(7 + H)
     x = torch.randn(N, C, H, H, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(K, C, R, R, generator=g) * (2.0 / (C * R * R)) ** 0.5).to(DEV, torch.bfloat16)
@@ -137,7 +138,7 @@ def test_conv_halo_fwd_matches_fp32_reference():
         y = lib().conv_halo_fwd(x, w)
         ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
         assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
-        # BN statistics epilogue (conv_fwd_bn's contract; it routes here under DTG_CONV_HALO=1)
+        # BN statistics epilogue (conv_fwd_bn's contract)
         y2, part = lib().conv_halo_fwd_bn(x, w)
         assert torch.equal(y2, y)
         p = part.view(-1, 2, 64).sum(0)

@@ -267,11 +267,19 @@ def test_mnist_cnn_trains_on_gpu():
     assert acc > 0.9, acc
 
 
+@pytest.fixture
+def forced_cfg():
+    """Force a GEMM tile configuration (csrc/kernels/gemm_forced*.hip; 99 = gemm8.hip) for one test."""
+    from dtg.ops._native import lib
+    yield lambda c: lib().gemm_force_cfg(c)
+    lib().gemm_force_cfg(0)
+
+
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 512), (1000, 520, 328), (512, 256, 4096)])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
-def test_gemm_big_tile_ring(M, N, K, a_kc, b_kc, monkeypatch):
-    """256x128 / 8-wave / 3-slot counted-vmcnt pipeline (forced on) vs fp32 torch."""
-    monkeypatch.setenv("DTG_GEMM_BIG", "1")
+def test_gemm_big_tile_ring(M, N, K, a_kc, b_kc, forced_cfg):
+    """256x128 / 8-wave / 3-slot counted-vmcnt pipeline (forced configuration 8) vs fp32 torch."""
+    forced_cfg(8)
     torch.manual_seed(0)
     A = torch.randn((M, K) if a_kc else (K, M), device="cuda").bfloat16()
     B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()
@@ -286,10 +294,10 @@ def test_gemm_big_tile_ring(M, N, K, a_kc, b_kc, monkeypatch):
 @pytest.mark.parametrize("M,N,K", [(512, 512, 64), (512, 768, 128), (1024, 512, 192), (768, 1024, 1024),
                                    (1000, 600, 328), (256, 256, 512)])
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, False), (False, True)])
-def test_gemm_8phase(M, N, K, a_kc, b_kc, monkeypatch):
-    """256x256 8-wave 8-phase kernel (forced on) vs fp32 torch: 1, 2, 3 and many K-tiles, ragged edges,
-    all four operand layouts, bias + GELU epilogue, split-K slabs."""
-    monkeypatch.setenv("DTG_GEMM8", "1")
+def test_gemm_8phase(M, N, K, a_kc, b_kc, forced_cfg):
+    """256x256 8-wave 8-phase kernel (forced configuration 99) vs fp32 torch: 1, 2, 3 and many K-tiles, ragged
+    edges, all four operand layouts, bias + GELU epilogue, split-K slabs."""
+    forced_cfg(99)
     torch.manual_seed(0)
     A = torch.randn((M, K) if a_kc else (K, M), device="cuda").bfloat16()
     B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()

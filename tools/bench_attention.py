@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Attention microbenchmark at the BERT-base shape: fused kernels (attention.hip) vs the unfused
-path (strided-batched MFMA GEMMs + softmax kernels).  Env DTG_ATTN_ABL=<bits> ablates parts of the
-fused backward (perf diagnosis only; results are then numerically meaningless)."""
+path (strided-batched MFMA GEMMs + softmax kernels)."""
 import argparse
 import json
 import os
@@ -42,7 +41,7 @@ def main():
     dout = torch.randn(B * S, H, device="cuda").bfloat16()
     L = lib()
     out, lse = L.attn_fused_fwd(qkv, mask, B, S, nh, a.p, 1)
-    r = {"shape": [B, S, nh], "abl": os.environ.get("DTG_ATTN_ABL", "0")}
+    r = {"shape": [B, S, nh]}
     r["fused_fwd_us"] = timeit(lambda: L.attn_fused_fwd(qkv, mask, B, S, nh, a.p, 1))
     r["fused_bwd_us"] = timeit(lambda: L.attn_fused_bwd(qkv, out, dout, lse, mask, B, S, nh, a.p, 1))
     cx, P, Pd = T.attention_fwd(qkv, mask, B, S, nh, a.p, 1)

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """BN-epilogue GEMMs at the ResNet-50 b512 1x1-conv shapes under the tile configuration forced by
-DTG_BN_GEMM_CFG (csrc/kernels/gemm.hip gemm_bn_dispatch; 0 = heuristic).  One JSON line per case:
+``--cfg`` (lib().gemm_bn_force_cfg, csrc/kernels/gemm.hip gemm_bn_dispatch; 0 = heuristic).  One JSON line per case:
 us per call and the rate over the compulsory HBM bytes.
 
-    for c in 0 1 2 3 4 5 6; do DTG_BN_GEMM_CFG=$c python tools/bn_gemm_ab.py; done
-    DTG_BN_AB_BATCH=1024 ... (the same shapes at per-GPU batch 1024)
+    for c in 0 1 2 3 4 5 6; do python tools/bn_gemm_ab.py --cfg $c; done
+    python tools/bn_gemm_ab.py --batch 1024 ... (the same shapes at per-GPU batch 1024)
 """
 import json
 import os
@@ -40,11 +40,17 @@ def timeit(fn, iters=10):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=512)
+    a = ap.parse_args()
     L = lib()
+    L.gemm_bn_force_cfg(a.cfg)
     dev = torch.device("cuda")
     bf = torch.bfloat16
-    cfg = os.environ.get("DTG_BN_GEMM_CFG", "0")
-    scale = int(os.environ.get("DTG_BN_AB_BATCH", "512")) // 512  # CASES are ResNet-50 b512 shapes
+    cfg = str(a.cfg)
+    scale = a.batch // 512  # CASES are ResNet-50 b512 shapes
     for mode, M, N, K in CASES:
         M *= scale
         A = torch.randn(M, K, device=dev, dtype=bf)

@@ -6,12 +6,3 @@ for hw in "56 64 64" "28 128 128" "14 256 256" "7 512 512"; do
     timeout -k 5 60 python tools/op_bench.py $op 256 $1 $2 $3 3 1
   done
 done 2>&1 | grep -v amdgpu.ids | tee gpurun_out/convsweep.txt
-for s in 1 2 3; do
- echo "DTG_CONV_STAGES=$s"
- for hw in "56 64 64" "14 256 256"; do
-  set -- $hw
-  for op in conv_fwd conv_dgrad conv_wgrad; do
-    DTG_CONV_STAGES=$s timeout -k 5 60 python tools/op_bench.py $op 256 $1 $2 $3 3 1
-  done
- done
-done 2>&1 | grep -v amdgpu.ids | tee -a gpurun_out/convsweep.txt

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: tests, benchmark, profile.  Every GPU step has its own time limit; a
 # crash/fault/timeout (exit >= 124 or signal) stops the session so nothing else touches the GPU.
-# Usage: tools/gpu_session.sh [steps...]   steps: test test_tf bench bench_bert bench_miopen prof prof_bert kbench smoke
+# Usage: tools/gpu_session.sh [steps...]   steps: test test_tf bench bench_bert prof prof_bert kbench smoke ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -32,7 +32,6 @@ for s in "$@"; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_pg) DTG_DDP_FORCE=1 run bench_pg 600 python bench.py --steps 20 --warmup 5 ;;
-    bench_pg_comm) DTG_DDP_FORCE=1 DTG_DDP_LAUNCH=comm run bench_pg_comm 600 python bench.py --steps 20 --warmup 5 ;;
     bench_pg_main) DTG_DDP_FORCE=1 DTG_WGRAD_STREAM=0 run bench_pg_main 600 python bench.py --steps 20 --warmup 5 ;;
     prof_pg) DTG_DDP_FORCE=1 run prof_pg 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pg -o run --output-format csv -- \
             python3 bench.py --steps 4 --warmup 3 ;;
@@ -41,10 +40,7 @@ for s in "$@"; do
     prof_emu) DTG_DDP_FORCE=1 DTG_COMM_EMULATE=${EMU:-100} run prof_emu 900 rocprofv3 --kernel-trace -d gpurun_out/prof_emu -o run \
             --output-format csv -- python3 bench.py --steps 6 --warmup 3 ;;
     test_resnet) run pytest_resnet 900 python -u -m pytest tests/test_resnet_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
-    bench_miopen) DTG_CONV_IMPL=miopen run bench_miopen 600 python bench.py --steps 20 --warmup 5 ;;
     kbench) run kbench 600 python tools/bench_kernels.py --json gpurun_out/kbench.json ;;
-    kbench_gemm_ab) DTG_GEMM_BIG=0 run kbench_small 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_small.json &&
-                    DTG_GEMM_BIG=1 run kbench_big 600 python tools/bench_kernels.py --only gemm --json gpurun_out/kbench_big.json ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
             python3 bench.py --steps 5 --warmup 3 ;;
     *) run "$(echo "$s" | tr -c 'A-Za-z0-9_.-' '_' | cut -c1-80)" 900 bash -c "$s < /dev/null" ;;
