@@ -1069,6 +1069,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
   m.def("gemm_bn_force_cfg", [](int64_t c) { dtg::gemm_bn_force_cfg((int)c); });
+  m.def("conv_force_tile", [](int64_t which, int64_t c) { dtg::conv_force_tile((int)which, (int)c); });
   m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });
   m.def("softmax_xent_bwd", &softmax_xent_bwd);
   m.def("gemm_pick_split", [](int64_t M, int64_t N, int64_t K, bool a_kc, int64_t target_wgs) {

@@ -381,7 +381,30 @@ void zero_(Tensor t) {
   dtg::fill_zero(t.data_ptr(), t.numel() * t.element_size(), cur_stream());
 }
 
+Tensor mul_bf16(Tensor a, Tensor b) {
+  CHECK_GPU_BF16_CONTIG(a);
+  CHECK_GPU_BF16_CONTIG(b);
+  TORCH_CHECK(a.sizes() == b.sizes(), "mul_bf16 shape mismatch");
+  TORCH_CHECK(((uintptr_t)a.data_ptr() % 16) == 0 && ((uintptr_t)b.data_ptr() % 16) == 0, "16-byte aligned");
+  c10::DeviceGuard dg(a.device());
+  auto out = at::empty_like(a);
+  dtg::mul_bf16(cbfp(a), cbfp(b), bfp(out), a.numel(), cur_stream());
+  return out;
+}
+
+Tensor mask_additive(Tensor mask) {
+  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask: contiguous GPU tensor");
+  TORCH_CHECK(mask.scalar_type() == at::kLong || mask.scalar_type() == at::kFloat, "mask int64 or fp32");
+  c10::DeviceGuard dg(mask.device());
+  auto out = at::empty(mask.sizes(), mask.options().dtype(at::kFloat));
+  dtg::mask_additive(mask.data_ptr(), mask.scalar_type() == at::kFloat, out.data_ptr<float>(), mask.numel(),
+                     cur_stream());
+  return out;
+}
+
 void register_transformer_ops(py::module_& m) {
+  m.def("mul_bf16", &mul_bf16);
+  m.def("mask_additive", &mask_additive);
   m.def("gemm_strided_batched", &gemm_strided_batched);
   m.def("ln_fwd", &ln_fwd, py::arg("h"), py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("eps") = 1e-12,
         py::arg("p_in") = 0.0, py::arg("seed_in") = 0, py::arg("p_out") = 0.0, py::arg("seed_out") = 0,

@@ -23,6 +23,9 @@ void adam_apply(float* w, bf16_t* mirror, void* grad, int grad_bf16, float* m, f
 void axpby(float* acc, const void* g, int g_bf16, long long n, float alpha, float beta, hipStream_t st);
 void f32_to_bf16(const float* x, bf16_t* y, long long n, hipStream_t st);
 void hyper_tick(float* hyper, hipStream_t st);
+// heads.hip: out = a * b (bf16); BERT additive key mask (1 - m) * -10000 from int64 / fp32 m
+void mul_bf16(const bf16_t* a, const bf16_t* b, bf16_t* out, long long n, hipStream_t st);
+void mask_additive(const void* mask, int is_f32, float* out, long long n, hipStream_t st);
 // zero `bytes` bytes at p (16-B aligned for the vector part) with a dtg kernel
 void fill_zero(void* p, long long bytes, hipStream_t st);
 
@@ -153,6 +156,7 @@ struct GemmBatch {
 // force one GEMM tile configuration (sweeps; 0 = heuristic, 99 = 8-phase 256x256)
 void gemm_force_cfg(int cfg);
 void gemm_bn_force_cfg(int cfg);
+void conv_force_tile(int which, int code);  // conv.hip: 0 fwd, 1 stride-1 dgrad
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
 int gemm_pick_split(int M, int N, int K, int a_kc = 0, int target_wgs = 0);  // target 0: default (512)
 void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,

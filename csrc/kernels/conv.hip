@@ -49,9 +49,9 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int s
 // C8: the input has exactly 8 (zero-padded) channels -- the ResNet stem, 3 -> 8 -- so one 16-B
 // chunk is one pixel and a 64-deep K step spans 8 (r, s) taps; K runs over (r, s, c) padded to a
 // multiple of 64 (taps rs >= R*S read the zero page; their weights are zero too).
-template <int ROWS, bool C8 = false>
+template <int ROWS, bool C8 = false, int NW = 4>
 struct FwdA {
-  static constexpr int PW = ROWS / 32;
+  static constexpr int PW = ROWS / (8 * NW);  // 8-row pieces per wave (one wave-instruction each)
   const bf16_t* x;
   const ConvGeom* g;
   int nbase[PW], ih0[PW], iw0[PW];
@@ -99,9 +99,9 @@ struct FwdA {
 };
 
 // ---- dgrad A: dy gathered at the input positions of the tile rows (KC), stride 1 ----------------
-template <int ROWS>
+template <int ROWS, int NW = 4>
 struct DgradA {
-  static constexpr int PW = ROWS / 32;
+  static constexpr int PW = ROWS / (8 * NW);
   const bf16_t* dy;
   const ConvGeom* g;
   int nbase[PW], ph0[PW], qw0[PW];
@@ -141,9 +141,9 @@ struct DgradA {
 };
 
 // ---- dgrad B: w as B[(r,s,k)][c] (MC: c contiguous) ---------------------------------------------
-template <int ROWS>
+template <int ROWS, int NW = 4>
 struct DgradB {
-  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / NW;
   const bf16_t* w;
   const ConvGeom* g;
   int col0;
@@ -168,9 +168,9 @@ struct DgradB {
 // A lane's columns (r, s, c) are the same at every K step (k0 advances by 64 rows and the MC swizzle
 // depends on the row within the tile only), so they are decomposed once in init(); a K step
 // decomposes only its rows m = k0 + kr into (n, p, q).
-template <int ROWS>
+template <int ROWS, int NW = 4>
 struct WgradB {
-  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / NW;
   const bf16_t* x;
   const ConvGeom* g;
   int M;
@@ -225,9 +225,9 @@ struct StrideClasses {
   StrideClass c[kMaxClasses];
 };
 
-template <int ROWS>
+template <int ROWS, int NW = 4>
 struct DgradSA {
-  static constexpr int PW = ROWS / 32;
+  static constexpr int PW = ROWS / (8 * NW);
   const bf16_t* dy;
   const ConvGeom* g;
   const StrideClass* sc;
@@ -269,9 +269,9 @@ struct DgradSA {
   }
 };
 
-template <int ROWS>
+template <int ROWS, int NW = 4>
 struct DgradSB {
-  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / 4;
+  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PW = 64 / KPI / NW;
   const bf16_t* w;
   const ConvGeom* g;
   const StrideClass* sc;
@@ -297,7 +297,7 @@ struct DgradSB {
 
 // ---------------------------------------------------------------------------------------------
 template <class CF, int BNMODE = 0, bool C8 = false>
-__global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
+__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) conv_fwd_kernel(ConvGeom G, const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
   const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = G.N * G.P * G.Q, Kd = C8 ? (G.R * G.S * 8 + 63) / 64 * 64 : G.R * G.S * G.C;  // C8: w is [K][Kd]
-  FwdA<CF::BM, C8> sa;
+  FwdA<CF::BM, C8, CF::NW> sa;
   sa.init(G, x, bm0, wave, lane);
   DenseKC<false> sb{w, (long long)Kd, G.K, Kd};
   f32x4 acc[4][4];
@@ -315,8 +315,8 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   mainloop_st<CF, true, true>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
-                              [&](lds_char* tl, int k0) { stage_kc<CF::BN>(sb, tl, bn0, k0, wave, lane); }, smem, 0,
-                              Kd, acc);
+                              [&](lds_char* tl, int k0) { stage_kc<CF::BN, DenseKC<false>, CF::NW>(sb, tl, bn0, k0, wave, lane); },
+                              smem, 0, Kd, acc);
   if constexpr (BNMODE != 0) {
     epilogue_bn<CF, BNMODE>(smem, acc, bm0, bn0, M, G.K, e, bn, t, [](int m) { return m; });
     return;
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(NT, 2) conv_fwd_kernel(ConvGeom G, const bf16_
 // so B is staged like the forward's weights (ds_read_b128) instead of through the MN-contiguous
 // [(r,s,k)][c] image and hardware-transposed reads
 template <class CF, int BNMODE = 0, bool WT = false>
-__global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
+__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) conv_dgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ w, Epi e, int tiles_n, BnEpi bn) {
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
   __shared__ __attribute__((aligned(16))) char smem_raw[CF::LDS_BYTES];
@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
   const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = G.N * G.H * G.W, Kd = G.R * G.S * G.K;
-  DgradA<CF::BM> sa;
+  DgradA<CF::BM, CF::NW> sa;
   sa.init(G, dy, bm0, wave, lane);
   f32x4 acc[4][4];
 #pragma unroll
@@ -347,10 +347,10 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
   if constexpr (WT) {
     DenseKC<true> sb{w, (long long)Kd, G.C, Kd};
     mainloop_st<CF, true, true>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
-                                [&](lds_char* tl, int k0) { stage_kc<CF::BN>(sb, tl, bn0, k0, wave, lane); }, smem,
-                                0, Kd, acc);
+                                [&](lds_char* tl, int k0) { stage_kc<CF::BN, DenseKC<true>, CF::NW>(sb, tl, bn0, k0, wave, lane); },
+                                smem, 0, Kd, acc);
   } else {
-    DgradB<CF::BN> sb{w, &G, bn0};
+    DgradB<CF::BN, CF::NW> sb{w, &G, bn0};
     mainloop_st<CF, true, false>([&](lds_char* tl, int k0) { sa(tl, k0, wave); },
                                  [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, 0, Kd, acc);
   }
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_kernel(ConvGeom G, const bf1
 }
 
 template <class CF>
-__global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
+__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) conv_wgrad_kernel(ConvGeom G, const bf16_t* __restrict__ dy,
                                                            const bf16_t* __restrict__ x, float* __restrict__ ws,
                                                            int tiles_n, int k_per_split) {
   static_assert(CF::BK == 64, "conv loaders stage 64-deep K steps");
@@ -378,14 +378,14 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
   const int Mo = G.K, No = G.R * G.S * G.C;   // output dw [K][RSC]
   const int kbeg = split * k_per_split, kend = min(M, kbeg + k_per_split);
   DenseMC<true> sa{dy, (long long)G.K, G.K, M};
-  WgradB<CF::BN> sb;
+  WgradB<CF::BN, CF::NW> sb;
   sb.init(x, G, bn0, M, wave, lane);
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  mainloop_st<CF, false, false>([&](lds_char* tl, int k0) { stage_mc<CF::BM>(sa, tl, bm0, k0, wave, lane); },
+  mainloop_st<CF, false, false>([&](lds_char* tl, int k0) { stage_mc<CF::BM, DenseMC<true>, CF::NW>(sa, tl, bm0, k0, wave, lane); },
                                 [&](lds_char* tl, int k0) { sb(tl, k0, wave, lane); }, smem, kbeg, kend, acc);
   float* slab = ws + (long long)split * Mo * No;
   epilogue_staged<CF>(smem, acc, bm0, bn0, Mo, No, [&](int m, int n, float (&v)[8]) {
@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(NT, 2) conv_wgrad_kernel(ConvGeom G, const bf1
 }
 
 template <class CF, int BNMODE = 0>
-__global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideClasses SC,
+__global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) conv_dgrad_s_kernel(ConvGeom G, StrideClasses SC,
                                                              const bf16_t* __restrict__ dy,
                                                              const bf16_t* __restrict__ w, Epi e, int tiles_n,
                                                              BnEpi bn) {
@@ -407,9 +407,9 @@ __global__ void __launch_bounds__(NT, 2) conv_dgrad_s_kernel(ConvGeom G, StrideC
   const int bm0 = (t / tiles_n) * CF::BM, bn0 = (t % tiles_n) * CF::BN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = G.N * S.Hc * S.Wc, Kd = S.nr * S.ns * G.K;
-  DgradSA<CF::BM> sa;
+  DgradSA<CF::BM, CF::NW> sa;
   sa.init(G, S, dy, bm0, wave, lane);
-  DgradSB<CF::BN> sb{w, &G, &S, bn0};
+  DgradSB<CF::BN, CF::NW> sb{w, &G, &S, bn0};
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -450,6 +450,23 @@ void conv_set_stages(int which, int stages) {  // 0 restores the measured defaul
   if (which >= 0 && which < 3) g_conv_stages[which] = stages >= 1 && stages <= 3 ? stages : -1;
 }
 
+// Output tile forced per pass (fwd, dgrad) for A/B tools (conv_force_tile; tools/conv_tile_ab.py): 0 = the
+// heuristics; 1 = 128x256, 8 waves, register-pipelined; 2 = 256x128, 8 waves, RP; 3 = 128x256, 8 waves, single
+// stage.  Wider output tiles re-read the gathered input through L2 once per 256 output channels instead of 128.
+static int g_conv_tile[2] = {0, 0};
+void conv_force_tile(int which, int code) {
+  if (which >= 0 && which < 2) g_conv_tile[which] = code;
+}
+template <class F>
+static bool run_forced_tile(int which, F&& run) {
+  switch (g_conv_tile[which]) {
+    case 1: run(Cfg<128, 256, 1, 8, 64, true>()); return true;
+    case 2: run(Cfg<256, 128, 1, 8, 64, true>()); return true;
+    case 3: run(Cfg<128, 256, 1, 8>()); return true;
+    default: return false;
+  }
+}
+
 template <int BM, int BN, class F>
 static void run_sched(int sched, F&& run) {
   if (sched == 1) run(Cfg<BM, BN, 1>());
@@ -473,9 +490,10 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 1) { conv_fwd_kernel<CF, 1><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else { conv_fwd_kernel<CF><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    if (bn.mode == 1) { conv_fwd_kernel<CF, 1><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_fwd_kernel<CF><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
+  if (run_forced_tile(0, run)) return;
   const int sc = conv_stages(0, M, K, R * S * C);
   if (conv_skinny(K)) run_sched<256, 64>(sc, run);
   else run_sched<128, 128>(sc, run);
@@ -490,8 +508,8 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (K + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 1) { conv_fwd_kernel<CF, 1, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else { conv_fwd_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    if (bn.mode == 1) { conv_fwd_kernel<CF, 1, true><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_fwd_kernel<CF, 0, true><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   if (conv_skinny(K)) run(Cfg<256, 64, 1>());
   else run(Cfg<128, 128, 1>());
@@ -553,9 +571,9 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
   const int sc = conv_stages(1, (long long)max_tiles * BM / tn, G.C, G.R * G.S * G.K / (s * s));
   auto run = [&](auto cf) {
     using CF = decltype(cf);
-    if (bn.mode == 2) { conv_dgrad_s_kernel<CF, 2><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else if (bn.mode == 3) { conv_dgrad_s_kernel<CF, 3><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else { conv_dgrad_s_kernel<CF><<<grid, NT, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    if (bn.mode == 2) { conv_dgrad_s_kernel<CF, 2><<<grid, CF::NTH, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else if (bn.mode == 3) { conv_dgrad_s_kernel<CF, 3><<<grid, CF::NTH, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_dgrad_s_kernel<CF><<<grid, CF::NTH, 0, st>>>(G, SC, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
   if (skinny) run_sched<256, 64>(sc, run);
   else run_sched<128, 128>(dgrad_sched(sc, G), run);
@@ -571,23 +589,12 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
   auto run = [&](auto cf) {
     using CF = decltype(cf);
     const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 2) { conv_dgrad_kernel<CF, 2><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else if (bn.mode == 3) { conv_dgrad_kernel<CF, 3><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else { conv_dgrad_kernel<CF><<<tm * tn, NT, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    if (bn.mode == 2) { conv_dgrad_kernel<CF, 2><<<tm * tn, CF::NTH, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else if (bn.mode == 3) { conv_dgrad_kernel<CF, 3><<<tm * tn, CF::NTH, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
+    else { conv_dgrad_kernel<CF><<<tm * tn, CF::NTH, 0, st>>>(G, dy, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
-  auto run_t = [&](auto cf) {  // K-contiguous transposed weights
-    using CF = decltype(cf);
-    const int tn = (C + CF::BN - 1) / CF::BN, tm = (M + CF::BM - 1) / CF::BM;
-    if (bn.mode == 2) { conv_dgrad_kernel<CF, 2, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else if (bn.mode == 3) { conv_dgrad_kernel<CF, 3, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
-    else { conv_dgrad_kernel<CF, 0, true><<<tm * tn, NT, 0, st>>>(G, dy, wT, e, tn, bn); DTG_LAUNCH_CHECK(); }
-  };
+  if (run_forced_tile(1, run)) return 1;
   const int sc = conv_stages(1, M, C, R * S * K);
-  if (wT && sc == 1) {
-    if (conv_skinny(C)) run_t(Cfg<256, 64, 1>());
-    else run_t(Cfg<128, 128, 1>());
-    return 1;
-  }
   if (conv_skinny(C)) run_sched<256, 64>(sc, run);
   else run_sched<128, 128>(dgrad_sched(sc, G), run);
   return 1;
@@ -622,7 +629,7 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
     using CF = decltype(cf);
     const int tn = (No + CF::BN - 1) / CF::BN, tm = (K + CF::BM - 1) / CF::BM;
     dim3 grid(tm * tn, split);
-    conv_wgrad_kernel<CF><<<grid, NT, 0, st>>>(G, dy, x, ws, tn, kps); DTG_LAUNCH_CHECK();
+    conv_wgrad_kernel<CF><<<grid, CF::NTH, 0, st>>>(G, dy, x, ws, tn, kps); DTG_LAUNCH_CHECK();
   };
   const int sc = conv_stages(2);
   if (K <= 64) run_sched<64, 256>(sc, run);  // 64 output channels: one 64-row tile

@@ -340,4 +340,42 @@ void emb_word_bwd_owned(const bf16_t* ds, const long long* ids, bf16_t* gW, int 
                      V); DTG_LAUNCH_CHECK();
 }
 
+// ---- small BERT step helpers on dtg kernels (no framework elementwise launches on the step) ------------------
+// out = a * b, bf16, 8 elements per lane (the MLM head's gelu'(pre) multiply)
+__global__ void __launch_bounds__(256) mul_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                       bf16_t* __restrict__ out, long long n) {
+  const long long nvec = n >> 3;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long v = (long long)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    float x[8], y[8];
+    load8_bf16(a + (v << 3), x);
+    load8_bf16(b + (v << 3), y);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] *= y[k];
+    store8_bf16(out + (v << 3), x);
+  }
+  if (blockIdx.x == 0)
+    for (long long i = (nvec << 3) + threadIdx.x; i < n; i += blockDim.x) out[i] = f2bf(bf2f(a[i]) * bf2f(b[i]));
+}
+
+void mul_bf16(const bf16_t* a, const bf16_t* b, bf16_t* out, long long n, hipStream_t st) {
+  if (n <= 0) return;
+  mul_bf16_kernel<<<grid_for((n >> 3) + 1, 256, 4096), 256, 0, st>>>(a, b, out, n); DTG_LAUNCH_CHECK();
+}
+
+// additive key mask: (1 - mask) * -10000 as fp32, from an int64 or fp32 [B, S] 1/0 mask (BERT)
+template <class T>
+__global__ void __launch_bounds__(256) mask_additive_kernel(const T* __restrict__ m, float* __restrict__ out, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (1.f - (float)m[i]) * -10000.f;
+}
+
+void mask_additive(const void* mask, int is_f32, float* out, long long n, hipStream_t st) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, 256, 4096);
+  if (is_f32) mask_additive_kernel<float><<<grid, 256, 0, st>>>((const float*)mask, out, n);
+  else mask_additive_kernel<long long><<<grid, 256, 0, st>>>((const long long*)mask, out, n);
+  DTG_LAUNCH_CHECK();
+}
+
 }  // namespace dtg

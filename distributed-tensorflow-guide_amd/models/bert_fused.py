@@ -217,7 +217,7 @@ class _MLMFn(torch.autograd.Function):
         gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
         dt = gemm(dl, True, word, False)                               # [P, H]
         da, _ = L.ln_bwd(dt, a, g, mean, rstd, gg, gb, 0.0, 0, 0.0, 0, False)
-        dpre = torch.mul(da, pre)                                      # pre holds gelu'(pre-activation)
+        dpre = L.mul_bf16(da, pre)                                     # pre holds gelu'(pre-activation)
         L.colsum(dpre, gbt, True)
         gemm(dpre, False, hm, False, out=gwt, beta=1.0)
         dhm = gemm(dpre, True, w_t, False)
@@ -282,7 +282,7 @@ class _HeadsFn(torch.autograd.Function):
         gemm(dl, False, t, False, out=gword, beta=1.0)                 # tied decoder: dWemb += dl^T t
         dt = gemm(dl, True, word, False)
         da, _ = L.ln_bwd(dt, a, g, mean, rstd, gg, gb, 0.0, 0, 0.0, 0, False)
-        dpre = torch.mul(da, pre)                                      # pre holds gelu'(pre-activation)
+        dpre = L.mul_bf16(da, pre)                                     # pre holds gelu'(pre-activation)
         L.colsum(dpre, gbt, True)
         gemm(dpre, False, hm, False, out=gwt, beta=1.0)
         dhm = gemm(dpre, True, w_t, False)

@@ -76,6 +76,8 @@ def attention_ref(qkv, mask_add, B, S, nh, p=0.0, seed=0):
 
 def mask_additive(attention_mask):
     """[B, S] 1/0 attention mask -> fp32 additive key mask (0 / -10000, as in BERT)."""
+    if attention_mask.is_cuda and attention_mask.dtype in (torch.int64, torch.float32):
+        return lib().mask_additive(attention_mask.contiguous())  # one dtg kernel
     return (1.0 - attention_mask.float()) * -10000.0
 
 
