@@ -25,9 +25,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
-// pack two floats into one dword of 2x bf16 (lo in low half)
+// pack two floats into one dword of 2x bf16 (lo in low half): ONE v_cvt_pk_bf16_f32 with both sources (two
+// scalar conversions cost a convert each plus a shift and an or)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const bf16x2v b = __builtin_convertvector((f32x2v){lo, hi}, bf16x2v);
+  return __builtin_bit_cast(uint32_t, b);
 }
 
 struct alignas(16) u32x4 { uint32_t x, y, z, w; };

@@ -185,6 +185,7 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
   if (const int fc = forced_cfg()) {
+    if (fc == 98 && bt.count == 1 && split_k == 1 && gemm8p_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, st)) return;
     if (fc == 99 && bt.count == 1) {
       gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
       return;

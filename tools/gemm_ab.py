@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
     ap.add_argument("--splits", default="0", help="comma list of split_k values to try (0 = heuristic)")
+    ap.add_argument("--epi", default="none", choices=["none", "bias", "gelu", "dgelu"],
+                    help="dtg epilogue: bias; bias + GELU with GELU' saved (BERT FFN1 forward); x saved GELU' "
+                         "(FFN2 data gradient).  hipBLASLt ('lib') always runs the plain GEMM")
     a = ap.parse_args()
     L = lib()
     dev = torch.device("cuda")
@@ -55,11 +58,14 @@ def main():
         Ct = torch.empty(M, N, device=dev, dtype=torch.bfloat16)  # hipBLASLt: bf16 out
         flops = 2.0 * M * N * K
         cfgs = [(int(c), int(sp)) for c in a.cfgs.split(",") for sp in a.splits.split(",")]
+        bias = torch.randn(N, device=dev) if a.epi in ("bias", "gelu") else None
+        aux = (torch.rand(M, N, device=dev) + 0.5).bfloat16() if a.epi in ("gelu", "dgelu") else None
+        act, aux_mode = {"none": (0, 0), "bias": (0, 0), "gelu": (2, 3), "dgelu": (0, 4)}[a.epi]
 
         def run_cfg(cs):
             c, sp = cs
             L.gemm_force_cfg(c)
-            L.gemm(A, akc, B, bkc, C, 1.0, 0.0, None, 0, sp)
+            L.gemm(A, akc, B, bkc, C, 1.0, 0.0, bias, act, sp, aux, aux_mode)
 
         times = {c: [] for c in cfgs}
         times["lib"] = []
@@ -83,7 +89,7 @@ def main():
             res[str(c)] = {"us_med": round(ts[len(ts) // 2], 1), "us_min": round(ts[0], 1),
                            "tflops": round(flops / ts[len(ts) // 2] / 1e6, 1)}
         # correctness of each dtg config against hipBLASLt
-        ref = torch.matmul(At.float(), Bt.float()) if M * N * K <= 2 ** 36 else None
+        ref = torch.matmul(At.float(), Bt.float()) if M * N * K <= 2 ** 36 and a.epi == "none" else None
         if ref is not None:
             for c in cfgs:
                 run_cfg(c)

@@ -2,7 +2,7 @@
 """Run one native op on one shape repeatedly (for rocprofv3 --pmc passes and A/B timing).
 
     python tools/op_bench.py gemm_bn1 802816 256 64        # M N K  (A [M,K] x W[N,K]^T + BN stats)
-    python tools/op_bench.py gemm 802816 256 64            # plain forward GEMM
+    python tools/op_bench.py gemm 802816 256 64            # plain forward GEMM (GEMM_CFG=98: forced tile config)
     python tools/op_bench.py conv_fwd_bn 256 56 64 64 3 1  # N H C K R stride (pad R//2)
     python tools/op_bench.py conv_dgrad_bn 256 14 256 256 3 1
     python tools/op_bench.py conv_wgrad 256 14 256 256 3 1
@@ -23,6 +23,8 @@ def main():
     a = [int(v) for v in sys.argv[2:]]
     iters = int(os.environ.get("ITERS", "20"))
     L = lib()
+    if os.environ.get("GEMM_CFG"):  # forced GEMM tile configuration (gemm_force_cfg), e.g. 98 = persistent 256x256
+        L.gemm_force_cfg(int(os.environ["GEMM_CFG"]))
     dev = torch.device("cuda")
     bf = torch.bfloat16
     if op in ("gemm", "gemm_bn1"):
