@@ -185,7 +185,9 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
   if (const int fc = forced_cfg()) {
-    if (fc == 98 && bt.count == 1 && split_k == 1 && gemm8p_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, st)) return;
+    if (fc >= 96 && fc <= 98 && bt.count == 1 && split_k == 1 &&
+        gemm8p_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, st, 98 - fc))
+      return;
     if (fc == 99 && bt.count == 1) {
       gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
       return;
@@ -271,7 +273,9 @@ static void launch_bn_cfg(const bf16_t* A, long long lda, const bf16_t* B, long 
 }
 
 // gemm_bn_force_cfg (tools/bn_gemm_ab.py) forces the BN-epilogue GEMM tile: 1 128x128, 2 64x256, 3 128x128
-// register-pipelined, 4 256x64, 5 128x256 8 waves, 6 256x128 8 waves; 0 = the heuristic below
+// register-pipelined, 4 256x64, 5 128x256 8 waves, 6 256x128 8 waves; 0 = the heuristic below (mode 1: the streaming
+// expand kernel first, gemm_expand.hip, where it applies); -1 = the heuristic without the expand kernel; -2 / -3 =
+// expand kernel variants 1 / 2 (non-temporal stores / 3 workgroups per CU)
 static int g_bn_gemm_cfg = 0;
 void gemm_bn_force_cfg(int cfg) { g_bn_gemm_cfg = cfg; }
 
@@ -324,12 +328,21 @@ static void gemm_bn_xa_dispatch(const bf16_t* A, long long lda, const bf16_t* B,
   else launch_bn_xa<Cfg<128, 128, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
+// gemm_expand.hip: persistent streaming GEMM + statistics for short-K, wide-N forward 1x1 convs
+bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long ldw, bf16_t* C, long long ldc, int M,
+                    int N, int K, float* part, hipStream_t st, int variant);
+
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   Epi e{C, ldc, 1, 1.f, bn.mode == 3 ? beta : 0.f, nullptr, 0};
   if (bn.mode == 1 && bn.xcoef) gemm_bn_xa_dispatch(A, lda, B, ldb, M, N, K, e, bn, st);
-  else if (bn.mode == 1) gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
+  else if (bn.mode == 1) {
+    if ((g_bn_gemm_cfg == 0 || g_bn_gemm_cfg <= -2) &&
+        gemm_expand_bn(A, lda, B, ldb, C, ldc, M, N, K, bn.part, st, g_bn_gemm_cfg == 0 ? 0 : -1 - g_bn_gemm_cfg))
+      return;
+    gemm_bn_dispatch<1>(A, lda, B, ldb, M, N, K, e, bn, st);
+  }
   else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.x2) gemm_bn_dispatch<4>(A, lda, B, ldb, M, N, K, e, bn, st);
   else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);

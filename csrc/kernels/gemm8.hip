@@ -348,7 +348,9 @@ __device__ __forceinline__ void mul_raw8(float (&v)[8], const u32x4v& w) {
 
 }  // namespace g8
 
-template <bool BKC, int EM>
+// ABL (timing ablations for tools/gemm_ab.py only, results are garbage): 1 = no operand DMA after the
+// prologue, 2 = no barriers inside the K loop
+template <bool BKC, int EM, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict__ A, long long lda,
                                                         const bf16_t* __restrict__ B, long long ldb, int K,
                                                         int tiles_n, int tiles, Epi e) {
@@ -404,6 +406,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
   tile_rc(0, cur_bm, cur_bn);
   tile_rc(1, nxt_bm, nxt_bn);
   auto stA = [&](int u, int d, int h) {
+    if constexpr (ABL == 1) { if (u > 0) return; }
     const int k = kk + d;
     const int bm = k < nk ? cur_bm : nxt_bm, k0 = (k < nk ? k : k - nk) * BK;
     const char* sb = (const char*)(A + (long long)bm * lda + k0);
@@ -414,6 +417,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
                                        0, 0);
   };
   auto stB = [&](int u, int d, int h) {
+    if constexpr (ABL == 1) { if (u > 0) return; }
     const int k = kk + d;
     const int bn = k < nk ? cur_bn : nxt_bn, k0 = (k < nk ? k : k - nk) * BK;
     lds_char* t = B_h(u + d, h);
@@ -445,6 +449,10 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
         __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], AF[i][ks], acc[I0 + i][J0 + j], 0, 0, 0);     \
   }
 
+#define DTG_G8P_BAR()                                   \
+  do {                                                  \
+    if constexpr (ABL != 2) __builtin_amdgcn_s_barrier(); \
+  } while (0)
   if (U > 0) {
     stA(0, 0, 0);
     stB(0, 0, 0);
@@ -479,7 +487,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
                                              (lds_void*)(smem + BIAS_OFF + ((ti & 1) * 8 + wave) * 256), 4, 0, 0);
         }
         if (n1) stA(u, 1, 1);
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (asm-read operands)
         __builtin_amdgcn_s_setprio(1);
@@ -488,7 +496,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
         if (!n1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else if (post) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + EPI_VM) : "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
       }
       // ---- P1: quadrant (1,0)
       {
@@ -498,13 +506,13 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) a1[i][ks] = g8::hfrag<AKC>(ta, wr * 64 + i * 16, ks, lane);
         if (n1) stB(u, 1, 1);
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (asm-read operands)
         __builtin_amdgcn_s_setprio(1);
         DTG_G8P_QUAD(4, 0, a1)
         __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
       }
       // ---- P2: quadrant (1,1)
       {
@@ -514,7 +522,7 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) b[j][ks] = g8::bfrag_perm<BKC>(tb, wc * 32, j, ks, lane);
         if (n2) stA(u, 2, 0);
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs below the wait (asm-read operands)
         __builtin_amdgcn_s_setprio(1);
@@ -523,18 +531,18 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
         if (!n2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else if (post) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + EPI_VM) : "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
       }
       // ---- P3: quadrant (0,1)
       {
         if (n2) stB(u, 2, 0);
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
         __builtin_amdgcn_s_setprio(1);
         DTG_G8P_QUAD(0, 2, a0)
         __builtin_amdgcn_s_setprio(0);
         if (n2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        DTG_G8P_BAR();
       }
       post = false;
       // ---- tile finished: epilogue from registers while the next tile's first K-tiles stream in
@@ -583,17 +591,18 @@ __global__ void __launch_bounds__(512, 1) gemm8p_kernel(const bf16_t* __restrict
       }
     }
 #undef DTG_G8P_QUAD
+#undef DTG_G8P_BAR
     if (wr == 0) __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- host ----------------------------------------------------------------------------------------
-template <bool BK_, int EM>
+template <bool BK_, int EM, int ABL = 0>
 static void launch8p(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                      const Epi& e, hipStream_t st) {
   const int tiles_n = N / g8::BN, tiles = (M / g8::BM) * tiles_n;
-  hipLaunchKernelGGL((gemm8p_kernel<BK_, EM>), dim3(256), dim3(g8::NTH), 0, st, A, lda, B, ldb, K, tiles_n, tiles, e);
+  hipLaunchKernelGGL((gemm8p_kernel<BK_, EM, ABL>), dim3(256), dim3(g8::NTH), 0, st, A, lda, B, ldb, K, tiles_n, tiles, e);
   DTG_LAUNCH_CHECK();
 }
 
@@ -614,13 +623,19 @@ int gemm8p_mode(const Epi& e) {
 }
 
 bool gemm8p_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, const Epi& e,
-                 int M, int N, int K, hipStream_t st) {
+                 int M, int N, int K, hipStream_t st, int abl) {
   const int em = gemm8p_mode(e);
   if (em < 0 || !a_kc || M % g8::BM || N % g8::BN || K % BK || K < 2 * BK || (lda & 7) || (ldb & 7)) return false;
   // per-lane chunk offsets are 32-bit byte offsets from the tile base (at most 256 rows / 64 k-rows of a
   // leading dimension)
   if (256LL * lda * 2 >= (1LL << 31) || 256LL * ldb * 2 >= (1LL << 31)) return false;
   if ((long long)(M / g8::BM) * (N / g8::BN) < 256) return false;  // fewer tiles than CUs: not persistent work
+  if (abl) {  // timing ablations: plain epilogue, KC B only
+    if (em != 0 || !b_kc) return false;
+    if (abl == 1) launch8p<true, 0, 1>(A, lda, B, ldb, M, N, K, e, st);
+    else launch8p<true, 0, 2>(A, lda, B, ldb, M, N, K, e, st);
+    return true;
+  }
   switch (em) {
     case 0: launch8p_b<0>(b_kc, A, lda, B, ldb, M, N, K, e, st); break;
     case 1: launch8p_b<1>(b_kc, A, lda, B, ldb, M, N, K, e, st); break;

@@ -55,6 +55,34 @@ def test_gemm_bn_fwd_stats(M, N, K):
     assert _rel(q, (of * of).sum(0)) < 1e-3
 
 
+# the persistent streaming expand kernel (csrc/kernels/gemm_expand.hip: K in {64, 128}, N % 256 == 0, M % 64 == 0,
+# M * N >= 2^24): one, two and four 256-column slices, a row-block count that does not divide the grid
+@pytest.mark.parametrize("M,N,K", [(65536, 256, 64), (32768, 512, 128), (64 * 1031, 256, 64), (16384, 1024, 64),
+                                   (20480, 1024, 128)])
+def test_gemm_bn_expand_stats(M, N, K):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(N, K, generator=g).mul_(K ** -0.5).to(dev, torch.bfloat16)
+    L = lib()
+    out, part = L.gemm_bn(a, w, 1)
+    ref = a.float() @ w.float().t()
+    assert _rel(out, ref) < 1e-2
+    s, q = _bn_stats(part, N)
+    of = out.float()
+    assert _rel(s, of.sum(0)) < 1e-4
+    assert _rel(q, (of * of).sum(0)) < 1e-4
+    # identical outputs to the tiled 128x128 path (same bf16 rounding of the same fp32 sums up to MFMA order)
+    L.gemm_bn_force_cfg(1)
+    try:
+        out1, part1 = L.gemm_bn(a, w, 1)
+    finally:
+        L.gemm_bn_force_cfg(0)
+    assert _rel(out, out1) < 2e-3
+    s1, q1 = _bn_stats(part1, N)
+    assert _rel(s, s1) < 1e-3 and _rel(q, q1) < 1e-4
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 64, 256), (2048, 128, 512), (1024, 256, 128), (1000, 192, 64)])
 def test_gemm_bn_bwd_stats(M, N, K):
     dev = torch.device("cuda")

@@ -12,7 +12,7 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do envs+=("$1"); shift; done
 mkdir -p gpurun_out
 for r in $(seq 1 "$rounds"); do
   for e in "${envs[@]}"; do
-    out=$(env $e timeout -k 10 300 python bench.py "$@" 2>gpurun_out/ab_err.log)
+    out=$(env $e timeout -k 10 300 python ${AB_SCRIPT:-bench.py} "$@" 2>gpurun_out/ab_err.log)
     rc=$?
     if [ $rc -ne 0 ]; then echo "[$e] rc=$rc"; tail -20 gpurun_out/ab_err.log; exit $rc; fi
     v=$(echo "$out" | python -c "import json,sys; d=json.loads([l for l in sys.stdin if l.startswith('{')][-1]); print(d['value'], d['ms_per_step'], d.get('allreduce_probe',''))")

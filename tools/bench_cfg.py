@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""bench.py with a forced native configuration, for in-step A/B runs (tools/ab_bench.sh takes environments,
+so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here before bench.py runs):
+
+    DTG_AB_BN_CFG=-1 python tools/bench_cfg.py [bench.py flags]     # BN-epilogue GEMMs without the expand kernel
+"""
+import os
+import runpy
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import dtg  # noqa: E402,F401
+from dtg.ops._native import lib  # noqa: E402
+
+if os.environ.get("DTG_AB_BN_CFG"):
+    lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
+if os.environ.get("DTG_AB_GEMM_CFG"):
+    lib().gemm_force_cfg(int(os.environ["DTG_AB_GEMM_CFG"]))
+sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[1:]
+runpy.run_path(sys.argv[0], run_name="__main__")

@@ -44,7 +44,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", type=int, default=0)
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--plain", action="store_true", help="also time the plain GEMM (no BN epilogue) per case")
+    ap.add_argument("--modes", default="1,2,3")
     a = ap.parse_args()
+    modes = {int(m) for m in a.modes.split(",")}
     L = lib()
     L.gemm_bn_force_cfg(a.cfg)
     dev = torch.device("cuda")
@@ -52,6 +55,8 @@ def main():
     cfg = str(a.cfg)
     scale = a.batch // 512  # CASES are ResNet-50 b512 shapes
     for mode, M, N, K in CASES:
+        if mode not in modes:
+            continue
         M *= scale
         A = torch.randn(M, K, device=dev, dtype=bf)
         ch = [torch.rand(N, device=dev) + 0.5 for _ in range(4)]
@@ -71,8 +76,15 @@ def main():
                 fn = lambda: L.gemm_bn(A, W, 2, x, *ch)  # noqa: E731
                 nbytes = 2 * (M * K + 2 * M * N)
         us = timeit(fn)
-        print(json.dumps({"cfg": int(cfg), "mode": mode, "M": M, "N": N, "K": K, "us": round(us, 1),
-                          "TBps": round(nbytes / us / 1e6, 2)}), flush=True)
+        rec = {"cfg": int(cfg), "mode": mode, "M": M, "N": N, "K": K, "us": round(us, 1),
+               "TBps": round(nbytes / us / 1e6, 2), "TFps": round(2.0 * M * N * K / us / 1e6, 1)}
+        if a.plain:
+            Wp = torch.randn(N, K, device=dev, dtype=bf)
+            C = torch.empty(M, N, device=dev, dtype=bf)
+            rec["plain_us"] = round(timeit(lambda: L.gemm(A, True, Wp, True, C, 1.0, 0.0, None, 0, 1)), 1)
+            rec["lib_us"] = round(timeit(lambda: torch.matmul(A, Wp.t(), out=C)), 1)
+            del Wp, C
+        print(json.dumps(rec), flush=True)
         del A, W
 
 
