@@ -810,9 +810,27 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> bn_fwd2_part(Tensor x, Tensor
 
 // dx, dx2 of two BNs fed by the same masked gradient dp (BN3 + projection BN), parameter gradients
 // accumulated into the given fp32 accumulators
+// fused weight gradient (both bn_bwd*_part): with `wact` [M, CI] (the input of the conv whose output is x) and
+// `wgrad` [C, CI] fp32, wgrad += dx^T wact inside the dx pass (bn_dx_wgrad.hip) -- check bn_dx_wgrad_ok first
+static void check_wgrad_fuse(const Tensor& x, const c10::optional<Tensor>& wact, const c10::optional<Tensor>& wgrad) {
+  TORCH_CHECK(wact.has_value() && wgrad.has_value() && wact->defined() && wgrad->defined(), "wact needs wgrad");
+  CHECK_CUDA(*wact);
+  CHECK_DT(*wact, at::kBFloat16);
+  CHECK_IN(*wgrad);
+  TORCH_CHECK(wgrad->scalar_type() == at::kFloat || wgrad->scalar_type() == at::kBFloat16, "wgrad fp32/bf16");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1), CI = (int)wact->size(1);
+  TORCH_CHECK(wact->dim() == 2 && wact->size(0) == M && wact->stride(1) == 1 && wact->stride(0) % 8 == 0 &&
+                  ((uintptr_t)wact->data_ptr() % 16) == 0,
+              "wact must be [M, CI] with 16-byte aligned rows");
+  TORCH_CHECK(wgrad->numel() == (long long)C * CI, "wgrad must be [C, CI]");
+  TORCH_CHECK(dtg::bn_dx_wgrad_ok(M, C, CI), "fused dx + wgrad: unsupported shape (see bn_dx_wgrad_ok)");
+}
+
 std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor gamma, Tensor smean, Tensor sinv,
                                         Tensor dgamma, Tensor dbeta, Tensor x2, Tensor part2, Tensor gamma2,
-                                        Tensor smean2, Tensor sinv2, Tensor dgamma2, Tensor dbeta2) {
+                                        Tensor smean2, Tensor sinv2, Tensor dgamma2, Tensor dbeta2,
+                                        c10::optional<Tensor> wact, c10::optional<Tensor> wgrad) {
   for (const Tensor* t : {&dp, &x, &x2}) {
     CHECK_IN(*t);
     CHECK_DT(*t, at::kBFloat16);
@@ -834,6 +852,22 @@ std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor
   c10::DeviceGuard dg(x.device());
   auto dx = at::empty_like(x), dx2 = at::empty_like(x);
   auto ws = at::empty({6LL * C}, x.options().dtype(at::kFloat));
+  if (wact.has_value() && wact->defined()) {
+    check_wgrad_fuse(x, wact, wgrad);
+    const int CI = (int)wact->size(1);
+    auto slabs = at::empty({(long long)dtg::bn_dx_wgrad_slabs(C, CI) * C * CI}, x.options().dtype(at::kFloat));
+    float* w = ws.data_ptr<float>();
+    dtg::bn_bwd_coef_from_part(part.data_ptr<float>(), gamma.data_ptr<float>(), smean.data_ptr<float>(),
+                               sinv.data_ptr<float>(), w, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), M, C, 1,
+                               cur_stream());
+    dtg::bn_bwd_coef_from_part(part2.data_ptr<float>(), gamma2.data_ptr<float>(), smean2.data_ptr<float>(),
+                               sinv2.data_ptr<float>(), w + 3LL * C, dgamma2.data_ptr<float>(),
+                               dbeta2.data_ptr<float>(), M, C, 1, cur_stream());
+    dtg::bn_dx_wgrad(cbfp(dp), cbfp(x), w, cbfp(x2), w + 3LL * C, bfp(dx), bfp(dx2), cbfp(*wact), wact->stride(0),
+                     wgrad->data_ptr(), wgrad->scalar_type() == at::kBFloat16, slabs.data_ptr<float>(), M, C, CI,
+                     cur_stream());
+    return {dx, dx2};
+  }
   dtg::bn_bwd2_from_part(cbfp(dp), cbfp(x), cbfp(x2), part.data_ptr<float>(), part2.data_ptr<float>(),
                          gamma.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
                          gamma2.data_ptr<float>(), smean2.data_ptr<float>(), sinv2.data_ptr<float>(), bfp(dx),
@@ -845,7 +879,9 @@ std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor
 std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp, Tensor x, Tensor part, Tensor gamma,
                                                                        Tensor smean, Tensor sinv, bool want_dres,
                                                                        c10::optional<Tensor> dgamma_acc,
-                                                                       c10::optional<Tensor> dbeta_acc) {
+                                                                       c10::optional<Tensor> dbeta_acc,
+                                                                       c10::optional<Tensor> wact,
+                                                                       c10::optional<Tensor> wgrad) {
   CHECK_IN(dp);
   CHECK_IN(x);
   CHECK_DT(dp, at::kBFloat16);
@@ -882,6 +918,19 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp,
     dbeta = at::empty({C}, fopt);
   }
   auto ws = at::empty({3LL * C}, fopt);
+  if (wact.has_value() && wact->defined()) {
+    TORCH_CHECK(!want_dres, "fused dx + wgrad: no dres");
+    check_wgrad_fuse(x, wact, wgrad);
+    const int CI = (int)wact->size(1);
+    auto slabs = at::empty({(long long)dtg::bn_dx_wgrad_slabs(C, CI) * C * CI}, fopt);
+    dtg::bn_bwd_coef_from_part(part.data_ptr<float>(), gamma.data_ptr<float>(), smean.data_ptr<float>(),
+                               sinv.data_ptr<float>(), ws.data_ptr<float>(), dgamma.data_ptr<float>(),
+                               dbeta.data_ptr<float>(), M, C, acc, cur_stream());
+    dtg::bn_dx_wgrad(cbfp(dp), cbfp(x), ws.data_ptr<float>(), nullptr, nullptr, bfp(dx), nullptr, cbfp(*wact),
+                     wact->stride(0), wgrad->data_ptr(), wgrad->scalar_type() == at::kBFloat16, slabs.data_ptr<float>(),
+                     M, C, CI, cur_stream());
+    return {dx, dres, dgamma, dbeta};
+  }
   dtg::bn_bwd_from_part(cbfp(dp), cbfp(x), gamma.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
                         part.data_ptr<float>(), bfp(dx), want_dres ? bfp(*dres) : nullptr, dgamma.data_ptr<float>(),
                         dbeta.data_ptr<float>(), ws.data_ptr<float>(), M, C, acc, cur_stream());
@@ -995,7 +1044,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("beta") = 0.0, pybind11::arg("split_k") = 0);
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
         pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
-  m.def("bn_bwd2_part", &bn_bwd2_part);
+  m.def("bn_bwd2_part", &bn_bwd2_part, pybind11::arg("dp"), pybind11::arg("x"), pybind11::arg("part"),
+        pybind11::arg("gamma"), pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("dgamma"),
+        pybind11::arg("dbeta"), pybind11::arg("x2"), pybind11::arg("part2"), pybind11::arg("gamma2"),
+        pybind11::arg("smean2"), pybind11::arg("sinv2"), pybind11::arg("dgamma2"), pybind11::arg("dbeta2"),
+        pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none());
+  m.def("bn_dx_wgrad_ok", [](int64_t M, int64_t C, int64_t CI) { return dtg::bn_dx_wgrad_ok(M, (int)C, (int)CI); });
   m.def("conv_halo_fwd_bn", &conv_halo_fwd_bn, pybind11::arg("x"), pybind11::arg("w"));
   m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("pooled") = false);
@@ -1013,7 +1067,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_part", &bn_fwd_part, pybind11::arg("x"), pybind11::arg("part"), pybind11::arg("res"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"),
         pybind11::arg("momentum"), pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("bits") = pybind11::none());
-  m.def("bn_bwd_part", &bn_bwd_part);
+  m.def("bn_bwd_part", &bn_bwd_part, pybind11::arg("dp"), pybind11::arg("x"), pybind11::arg("part"),
+        pybind11::arg("gamma"), pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("want_dres"),
+        pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none(),
+        pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none());
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("bn_dx_coef", &bn_dx_coef);
   m.def("bn_fold_weights", &bn_fold_weights);

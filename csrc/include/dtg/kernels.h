@@ -126,6 +126,14 @@ void bn_dx_from_coef(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_
 // Wab = [diag(a) W ; diag(bx) W] ([2K][N] bf16), cw = c^T W ([N] fp32) for coef = [a, bx, c] (batchnorm.hip)
 void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
                      hipStream_t st);
+// bn_dx_wgrad.hip: the dx pass (from bn_bwd_coef_from_part coefficients, optionally the projection shortcut's dx2
+// from the same dp) fused with the weight gradient dW += dx^T act of the conv that produced x (C x CI = 256 x 64 or
+// 512 x 128)
+bool bn_dx_wgrad_ok(long long M, int C, int CI);
+int bn_dx_wgrad_slabs(int C, int CI);
+void bn_dx_wgrad(const bf16_t* dp, const bf16_t* x, const float* coef, const bf16_t* x2, const float* coef2,
+                 bf16_t* dx, bf16_t* dx2, const bf16_t* act, long long ldact, void* wgrad, int wgrad_bf16,
+                 float* slabs, long long M, int C, int CI, hipStream_t st);
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
                       int C, int accum, hipStream_t st);

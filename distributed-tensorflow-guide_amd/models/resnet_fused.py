@@ -75,6 +75,11 @@ _BN2X = False
 # doubled-K dgrads took +3.4 ms and the side stream's dx passes (16 ms there) made it the critical path.  What
 # would remove them is a weight gradient reading [dp | y] with two accumulators (a_k G1 + bx_k G2 + c_k colsum x).
 _FOLD = False
+# _DXW = True: where the shape allows (stage 1: 256 x 64, bn_dx_wgrad_ok), conv3's weight gradient is computed inside
+# BN3's dx pass on the main stream (csrc/kernels/bn_dx_wgrad.hip) instead of re-reading dx on the side stream:
+# the backward is HBM-bound across both streams, and that re-read cost 0.3 ms of step per block
+# (profiles/r04_dx_wgrad).
+_DXW = True
 
 
 class _Bn3Link:
@@ -241,6 +246,10 @@ class _BottleneckFn(torch.autograd.Function):
         lk = ctx.link_out
         dyd = None
         coef3 = None  # set when BN3's backward is folded into the conv3 dgrad (_FOLD)
+        # conv3's weight gradient inside BN3's dx pass (_DXW)
+        w3_kw = (dict(wact=a2, wgrad=g[id(w3)].view(cout, width))
+                 if _DXW and a2 is not None and L.bn_dx_wgrad_ok(y3.shape[0], cout, width) else None)
+        w3_done = False
         if (lk is not None and lk.part is not None and do.data_ptr() == lk.dp.data_ptr()
                 and do.shape == lk.dp.shape):
             # block i+1 already masked dL/d out (do is dp) and reduced this BN's statistics
@@ -248,11 +257,14 @@ class _BottleneckFn(torch.autograd.Function):
                 bd = blk.down.bn
                 dy3, dyd = L.bn_bwd2_part(do, y3, lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)],
                                           sv[13], lk.part2, bd.weight, sv[14], sv[15], g[id(bd.weight)],
-                                          g[id(bd.bias)])
+                                          g[id(bd.bias)], **(w3_kw or {}))
+                w3_done = w3_kw is not None
             elif _FOLD and bits12_ok(ctx):
                 coef3 = L.bn_bwd_coef(lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)], y3.shape[0])
             else:
-                dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)])[0]
+                dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)],
+                                    **(w3_kw or {}))[0]
+                w3_done = w3_kw is not None
             dres = do  # our own buffer (pointer-checked above): dx accumulates into it in place
         else:
             for pt in ((lk.part, lk.part2) if lk is not None else ()):
@@ -283,6 +295,8 @@ class _BottleneckFn(torch.autograd.Function):
         elif coef3 is not None:
             with overlap.wgrad_scope(do, y3, coef3, a2):  # dy3 for the weight gradient only, off the main stream
                 _wgrad(L.bn_dx_coef(do, y3, coef3), a2, g[id(w3)].view(cout, width))
+        elif w3_done:
+            pass  # accumulated by BN3's dx pass above
         else:
             with overlap.wgrad_scope(dy3, a2):
                 _wgrad(dy3, a2, g[id(w3)].view(cout, width))

@@ -359,3 +359,45 @@ def test_bn_folded_dgrad(M, Kc, N, accum):
     # the side-stream half: dy from the same coefficients
     dy = L.bn_dx_coef(dp, y, coef)
     assert _rel(dy, dy_ref) < 1e-2
+
+
+@pytest.mark.parametrize("dual", [False, True])
+@pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,CI", [(256, 64), (512, 128)])
+def test_bn_dx_wgrad_fused(dual, gdtype, C, CI):
+    """BN backward dx pass fused with dW += dx^T act (csrc/kernels/bn_dx_wgrad.hip): dx equal to the unfused pass
+    up to fma contraction, dW against fp32 torch on the fused pass's bf16 dx, accumulated (beta = 1) into a fp32 or
+    bf16 gradient."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    M = 8192
+    L = lib()
+    assert L.bn_dx_wgrad_ok(M, C, CI) and not L.bn_dx_wgrad_ok(M, 2 * C, CI) and not L.bn_dx_wgrad_ok(M + 8, C, CI)
+    dp = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+    x = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+    x2 = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
+    act = torch.rand(M, CI, generator=g).to(dev, torch.bfloat16)
+
+    def chan():
+        mean, inv, gamma, _ = _chan(C, dev, g)
+        part = torch.zeros(SLOTS, 2, C, device=dev)
+        part[0, 0] = torch.randn(C, generator=g).to(dev) * 10
+        part[0, 1] = torch.randn(C, generator=g).to(dev) * 10
+        return mean, inv, gamma, part.view(-1)
+
+    m1, i1, g1, p1 = chan()
+    m2, i2, g2, p2 = chan()
+    w0 = (torch.randn(C, CI, generator=g) * 0.1).to(dev, gdtype)
+    wgrad = w0.clone()
+    z = lambda: torch.zeros(C, device=dev)  # noqa: E731
+    if dual:
+        ref = L.bn_bwd2_part(dp, x, p1.clone(), g1, m1, i1, z(), z(), x2, p2.clone(), g2, m2, i2, z(), z())
+        out = L.bn_bwd2_part(dp, x, p1.clone(), g1, m1, i1, z(), z(), x2, p2.clone(), g2, m2, i2, z(), z(),
+                             wact=act, wgrad=wgrad)
+        assert _rel(out[1], ref[1]) < 1e-3  # the same fp32 expression up to fma contraction, rounded to bf16
+    else:
+        ref = L.bn_bwd_part(dp, x, p1.clone(), g1, m1, i1, False, z(), z())
+        out = L.bn_bwd_part(dp, x, p1.clone(), g1, m1, i1, False, z(), z(), wact=act, wgrad=wgrad)
+    assert _rel(out[0], ref[0]) < 1e-3
+    want = w0.float() + out[0].float().t() @ act.float()
+    assert _rel(wgrad, want) < (1e-4 if gdtype == torch.float32 else 5e-3)

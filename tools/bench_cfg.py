@@ -3,6 +3,7 @@
 so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here before bench.py runs):
 
     DTG_AB_BN_CFG=-1 python tools/bench_cfg.py [bench.py flags]     # BN-epilogue GEMMs without the expand kernel
+    DTG_AB_SET=models.resnet_fused._DXW=0 python tools/bench_cfg.py  # a module switch (dtg.<module>.<name>=<int>)
 """
 import os
 import runpy
@@ -18,5 +19,10 @@ if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 if os.environ.get("DTG_AB_GEMM_CFG"):
     lib().gemm_force_cfg(int(os.environ["DTG_AB_GEMM_CFG"]))
+for item in filter(None, os.environ.get("DTG_AB_SET", "").split(",")):
+    path, val = item.split("=")
+    mod, name = path.rsplit(".", 1)
+    import importlib
+    setattr(importlib.import_module("dtg." + mod), name, type(getattr(importlib.import_module("dtg." + mod), name))(int(val)))
 sys.argv = [os.path.join(ROOT, "bench.py")] + sys.argv[1:]
 runpy.run_path(sys.argv[0], run_name="__main__")
