@@ -830,7 +830,8 @@ static void check_wgrad_fuse(const Tensor& x, const c10::optional<Tensor>& wact,
 std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor gamma, Tensor smean, Tensor sinv,
                                         Tensor dgamma, Tensor dbeta, Tensor x2, Tensor part2, Tensor gamma2,
                                         Tensor smean2, Tensor sinv2, Tensor dgamma2, Tensor dbeta2,
-                                        c10::optional<Tensor> wact, c10::optional<Tensor> wgrad) {
+                                        c10::optional<Tensor> wact, c10::optional<Tensor> wgrad,
+                                        c10::optional<Tensor> wact2, c10::optional<Tensor> wgrad2) {
   for (const Tensor* t : {&dp, &x, &x2}) {
     CHECK_IN(*t);
     CHECK_DT(*t, at::kBFloat16);
@@ -855,7 +856,14 @@ std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor
   if (wact.has_value() && wact->defined()) {
     check_wgrad_fuse(x, wact, wgrad);
     const int CI = (int)wact->size(1);
-    auto slabs = at::empty({(long long)dtg::bn_dx_wgrad_slabs(C, CI) * C * CI}, x.options().dtype(at::kFloat));
+    const bool w2 = wact2.has_value() && wact2->defined();
+    if (w2) {  // the projection shortcut's weight gradient too: dW2 += dx2^T wact2 (256 x 64 only)
+      check_wgrad_fuse(x2, wact2, wgrad2);
+      TORCH_CHECK(C == 256 && CI == 64 && wact2->size(1) == CI && wgrad2->scalar_type() == wgrad->scalar_type(),
+                  "wact2: 256 x 64 only, wgrad2 of wgrad's dtype");
+    }
+    const long long ns = (long long)dtg::bn_dx_wgrad_slabs(C, CI, w2) * C * CI;
+    auto slabs = at::empty({w2 ? 2 * ns : ns}, x.options().dtype(at::kFloat));
     float* w = ws.data_ptr<float>();
     dtg::bn_bwd_coef_from_part(part.data_ptr<float>(), gamma.data_ptr<float>(), smean.data_ptr<float>(),
                                sinv.data_ptr<float>(), w, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), M, C, 1,
@@ -865,7 +873,8 @@ std::tuple<Tensor, Tensor> bn_bwd2_part(Tensor dp, Tensor x, Tensor part, Tensor
                                dbeta2.data_ptr<float>(), M, C, 1, cur_stream());
     dtg::bn_dx_wgrad(cbfp(dp), cbfp(x), w, cbfp(x2), w + 3LL * C, bfp(dx), bfp(dx2), cbfp(*wact), wact->stride(0),
                      wgrad->data_ptr(), wgrad->scalar_type() == at::kBFloat16, slabs.data_ptr<float>(), M, C, CI,
-                     cur_stream());
+                     cur_stream(), w2 ? cbfp(*wact2) : nullptr, w2 ? wact2->stride(0) : 0,
+                     w2 ? wgrad2->data_ptr() : nullptr, w2 ? slabs.data_ptr<float>() + ns : nullptr);
     return {dx, dx2};
   }
   dtg::bn_bwd2_from_part(cbfp(dp), cbfp(x), cbfp(x2), part.data_ptr<float>(), part2.data_ptr<float>(),
@@ -1048,7 +1057,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("gamma"), pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("dgamma"),
         pybind11::arg("dbeta"), pybind11::arg("x2"), pybind11::arg("part2"), pybind11::arg("gamma2"),
         pybind11::arg("smean2"), pybind11::arg("sinv2"), pybind11::arg("dgamma2"), pybind11::arg("dbeta2"),
-        pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none());
+        pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none(),
+        pybind11::arg("wact2") = pybind11::none(), pybind11::arg("wgrad2") = pybind11::none());
   m.def("bn_dx_wgrad_ok", [](int64_t M, int64_t C, int64_t CI) { return dtg::bn_dx_wgrad_ok(M, (int)C, (int)CI); });
   m.def("conv_halo_fwd_bn", &conv_halo_fwd_bn, pybind11::arg("x"), pybind11::arg("w"));
   m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),

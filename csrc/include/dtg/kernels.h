@@ -130,10 +130,11 @@ void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* 
 // from the same dp) fused with the weight gradient dW += dx^T act of the conv that produced x (C x CI = 256 x 64 or
 // 512 x 128)
 bool bn_dx_wgrad_ok(long long M, int C, int CI);
-int bn_dx_wgrad_slabs(int C, int CI);
+int bn_dx_wgrad_slabs(int C, int CI, int w2 = 0);
 void bn_dx_wgrad(const bf16_t* dp, const bf16_t* x, const float* coef, const bf16_t* x2, const float* coef2,
                  bf16_t* dx, bf16_t* dx2, const bf16_t* act, long long ldact, void* wgrad, int wgrad_bf16,
-                 float* slabs, long long M, int C, int CI, hipStream_t st);
+                 float* slabs, long long M, int C, int CI, hipStream_t st, const bf16_t* act2 = nullptr,
+                 long long ldact2 = 0, void* wgrad2 = nullptr, float* slabs2 = nullptr);
 void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, const float* smean, const float* sinv,
                       const float* part, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta, float* ws, long long M,
                       int C, int accum, hipStream_t st);

@@ -80,6 +80,7 @@ _FOLD = False
 # the backward is HBM-bound across both streams, and that re-read cost 0.3 ms of step per block
 # (profiles/r04_dx_wgrad).
 _DXW = True
+_DXW2 = True  # ... and the stage-1 stride-1 projection's weight gradient in the dual form of that pass
 
 
 class _Bn3Link:
@@ -249,15 +250,20 @@ class _BottleneckFn(torch.autograd.Function):
         # conv3's weight gradient inside BN3's dx pass (_DXW)
         w3_kw = (dict(wact=a2, wgrad=g[id(w3)].view(cout, width))
                  if _DXW and a2 is not None and L.bn_dx_wgrad_ok(y3.shape[0], cout, width) else None)
-        w3_done = False
+        w3_done = wd_done = False
         if (lk is not None and lk.part is not None and do.data_ptr() == lk.dp.data_ptr()
                 and do.shape == lk.dp.shape):
             # block i+1 already masked dL/d out (do is dp) and reduced this BN's statistics
             if lk.part2 is not None:  # ... and the shortcut BN's: both dx in one pass over dp
                 bd = blk.down.bn
+                kw = dict(w3_kw or {})
+                if _DXW2 and w3_kw is not None and st == 1 and c == width == 64 and cout == 256:
+                    # the stride-1 projection's weight gradient in the same pass (dyd^T x, stage 1)
+                    kw.update(wact2=x2, wgrad2=g[id(blk.down.conv.weight)].view(cout, c))
+                    wd_done = True
                 dy3, dyd = L.bn_bwd2_part(do, y3, lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)],
                                           sv[13], lk.part2, bd.weight, sv[14], sv[15], g[id(bd.weight)],
-                                          g[id(bd.bias)], **(w3_kw or {}))
+                                          g[id(bd.bias)], **kw)
                 w3_done = w3_kw is not None
             elif _FOLD and bits12_ok(ctx):
                 coef3 = L.bn_bwd_coef(lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)], y3.shape[0])
@@ -336,8 +342,9 @@ class _BottleneckFn(torch.autograd.Function):
                                         g[id(bd.bias)])
             if st == 1:
                 dx2 = gemm(dyd, True, _mat(wd), False)
-                with overlap.wgrad_scope(dyd, x2):
-                    _wgrad(dyd, x2, g[id(wd)].view(cout, c))
+                if not wd_done:
+                    with overlap.wgrad_scope(dyd, x2):
+                        _wgrad(dyd, x2, g[id(wd)].view(cout, c))
             elif lk_in is not None:  # projection dgrad first, so the conv1 dgrad GEMM is the last writer
                 # only the even (h, w) rows of a stride-2 1x1 dgrad are written; the mode-3 GEMM below reads
                 # just those (sub2_hw) instead of a zero-filled full tensor

@@ -401,3 +401,28 @@ def test_bn_dx_wgrad_fused(dual, gdtype, C, CI):
     assert _rel(out[0], ref[0]) < 1e-3
     want = w0.float() + out[0].float().t() @ act.float()
     assert _rel(wgrad, want) < (1e-4 if gdtype == torch.float32 else 5e-3)
+
+
+def test_bn_dx_wgrad_fused_two_weights():
+    """Dual form with the projection shortcut's weight gradient too: dW += dx^T act, dW2 += dx2^T act2."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, C, CI = 8192, 256, 64
+    L = lib()
+    dp, x, x2 = (torch.randn(M, C, generator=g).to(dev, torch.bfloat16) for _ in range(3))
+    act, act2 = (torch.rand(M, CI, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    chans = []
+    for _ in range(2):
+        mean, inv, gamma, _ = _chan(C, dev, g)
+        part = torch.zeros(SLOTS, 2, C, device=dev)
+        part[0] = torch.randn(2, C, generator=g).to(dev) * 10
+        chans.append((mean, inv, gamma, part.view(-1)))
+    (m1, i1, g1, p1), (m2, i2, g2, p2) = chans
+    z = lambda: torch.zeros(C, device=dev)  # noqa: E731
+    w, w2 = torch.zeros(C, CI, device=dev), torch.zeros(C, CI, device=dev)
+    ref = L.bn_bwd2_part(dp, x, p1.clone(), g1, m1, i1, z(), z(), x2, p2.clone(), g2, m2, i2, z(), z())
+    out = L.bn_bwd2_part(dp, x, p1.clone(), g1, m1, i1, z(), z(), x2, p2.clone(), g2, m2, i2, z(), z(),
+                         wact=act, wgrad=w, wact2=act2, wgrad2=w2)
+    assert _rel(out[0], ref[0]) < 1e-3 and _rel(out[1], ref[1]) < 1e-3
+    assert _rel(w, out[0].float().t() @ act.float()) < 1e-4
+    assert _rel(w2, out[1].float().t() @ act2.float()) < 1e-4
