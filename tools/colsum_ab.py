@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B: dgrad GEMM (aux-mode-2 GELU backward) + separate column-sum kernel vs the fused colsum epilogue."""
+"""A/B: dgrad GEMM (aux-mode-4 GELU backward: x the saved GELU') + separate column-sum kernel vs the fused colsum epilogue."""
 import os
 import sys
 
@@ -17,9 +17,9 @@ for M, N, K in [(32768, 3072, 768), (8192, 3072, 768)]:
     pre = torch.randn(M, N, device=dev).bfloat16()
     d = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     cs = torch.zeros(N, device=dev)
-    fa = lambda: (L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 2), L.colsum(d, cs, True))  # noqa: E731
-    fb = lambda: L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 2, colsum=cs)  # noqa: E731
-    fc = lambda: L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 2)  # noqa: E731
+    fa = lambda: (L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 4), L.colsum(d, cs, True))  # noqa: E731
+    fb = lambda: L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 4, colsum=cs)  # noqa: E731
+    fc = lambda: L.gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 4)  # noqa: E731
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     res = {"sep": [], "fused": [], "gemm_only": []}
     for _ in range(5):
