@@ -76,9 +76,11 @@ void check_chan(const Tensor& t, int64_t C, const char* what) {
 }
 
 // y [N,H,W,C] (the stem conv output), part: its BN statistics partials (conv_fwd_c8 with_stats)
-// -> (pooled [N,P,Q,C], argmax uint8 [N,P,Q,C], save_mean [C], save_invstd [C]); running stats updated
+// -> (pooled [N,P,Q,C], argmax uint8 [N,P,Q,C], save_mean [C], save_invstd [C] [, y_am [N,P,Q,C]]); running
+// stats updated.  save_yam: also return y at each window's argmax, which lets stem_bn_pool_bwd run its statistics
+// pass over the pooled tensors
 std::vector<Tensor> stem_bn_pool_fwd(Tensor y, Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
-                                     double momentum, double eps, int64_t k, int64_t s, int64_t pad) {
+                                     double momentum, double eps, int64_t k, int64_t s, int64_t pad, bool save_yam) {
   check_nhwc8(y, "y");
   const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() &&
@@ -97,10 +99,13 @@ std::vector<Tensor> stem_bn_pool_fwd(Tensor y, Tensor part, Tensor gamma, Tensor
   auto out = at::empty({N, P, Q, C}, y.options());
   auto idx = at::empty({N, P, Q, C}, y.options().dtype(at::kByte));
   auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt), coef = at::empty({2LL * C}, fopt);
+  Tensor yam;
+  if (save_yam) yam = at::empty({N, P, Q, C}, y.options());
   dtg::stem_bn_pool_fwd(cbfp(y), part.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                         rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(),
                         coef.data_ptr<float>(), bfp(out), idx.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s, (int)pad,
-                        P, Q, (float)momentum, (float)eps, cur_stream());
+                        P, Q, (float)momentum, (float)eps, cur_stream(), save_yam ? bfp(yam) : nullptr);
+  if (save_yam) return {out, idx, smean, sinv, yam};
   return {out, idx, smean, sinv};
 }
 
@@ -123,7 +128,8 @@ Tensor stem_pack_pairs(Tensor x, int64_t pad, int64_t Wp) {
 // accumulated into the given fp32 buffers when both are passed, else returned fresh
 std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor gamma, Tensor beta, Tensor smean,
                                      Tensor sinv, int64_t k, int64_t s, int64_t pad,
-                                     c10::optional<Tensor> dgamma_acc, c10::optional<Tensor> dbeta_acc) {
+                                     c10::optional<Tensor> dgamma_acc, c10::optional<Tensor> dbeta_acc,
+                                     c10::optional<Tensor> yam) {
   check_nhwc8(dout, "dout");
   check_nhwc8(y, "y");
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dout.sizes() && idx.is_contiguous(),
@@ -136,6 +142,11 @@ std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor g
   TORCH_CHECK(k <= 2 * s && pad < k, "stem backward gathers at most 2x2 windows per pixel (k <= 2*stride)");
   for (auto* t : {&gamma, &beta, &smean, &sinv}) check_chan(*t, C, "per-channel tensor");
   const bool acc = dgamma_acc.has_value() && dgamma_acc->defined() && dbeta_acc.has_value() && dbeta_acc->defined();
+  const bool has_yam = yam.has_value() && yam->defined();
+  if (has_yam)
+    TORCH_CHECK(yam->is_cuda() && yam->scalar_type() == at::kBFloat16 && yam->sizes() == dout.sizes() &&
+                    yam->is_contiguous(),
+                "yam must be the forward's bf16 y-at-argmax tensor, shaped like dout");
   c10::DeviceGuard dg(y.device());
   auto fopt = y.options().dtype(at::kFloat);
   Tensor dgamma, dbeta;
@@ -153,7 +164,7 @@ std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor g
   dtg::stem_bn_pool_bwd(cbfp(dout), idx.data_ptr<uint8_t>(), cbfp(y), gamma.data_ptr<float>(), beta.data_ptr<float>(),
                         smean.data_ptr<float>(), sinv.data_ptr<float>(), bfp(dy), dgamma.data_ptr<float>(),
                         dbeta.data_ptr<float>(), acc ? 1 : 0, ws.data_ptr<float>(), N, H, W, C, (int)k, (int)s,
-                        (int)pad, P, Q, cur_stream());
+                        (int)pad, P, Q, cur_stream(), has_yam ? cbfp(*yam) : nullptr);
   return {dy, dgamma, dbeta};
 }
 
@@ -190,12 +201,16 @@ void register_pool_ops(pybind11::module_& m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
-  m.def("stem_bn_pool_fwd", &stem_bn_pool_fwd);
+  m.def("stem_bn_pool_fwd", &stem_bn_pool_fwd, pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("gamma"),
+        pybind11::arg("beta"), pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("momentum"),
+        pybind11::arg("eps"), pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("pad"),
+        pybind11::arg("save_yam") = false);
+  m.def("stem_pooled_stats_ok", &dtg::stem_pooled_stats_ok);
   m.def("stem_pack_pairs", &stem_pack_pairs, pybind11::arg("x"), pybind11::arg("pad"), pybind11::arg("Wp"));
   m.def("stem_bn_pool_bwd", &stem_bn_pool_bwd, pybind11::arg("dout"), pybind11::arg("idx"), pybind11::arg("y"),
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("smean"), pybind11::arg("sinv"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("pad"), pybind11::arg("dgamma_acc") = pybind11::none(),
-        pybind11::arg("dbeta_acc") = pybind11::none());
+        pybind11::arg("dbeta_acc") = pybind11::none(), pybind11::arg("yam") = pybind11::none());
   m.def("im2col", &im2col);
   m.def("col2im", &col2im);
 }

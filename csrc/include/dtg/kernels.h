@@ -248,8 +248,12 @@ void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t
 //      ws = stem_bwd_workspace_floats(N*H*W, C); dgamma/dbeta overwritten (accum = 0) or accumulated.
 void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, const float* beta, float* rmean,
                       float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
-                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st);
+                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st,
+                      bf16_t* yam = nullptr);
 long long stem_bwd_workspace_floats(long long M, int C);
+// the backward's statistics pass can run at pooled resolution (yam: y at each window's argmax, [N,P,Q,C],
+// written by stem_bn_pool_fwd when given) for these channel counts
+bool stem_pooled_stats_ok(int C);
 // channels_last [K, C, R, S] stem weights -> pixel-pair form [K][KP] (KP >= R * S2 * 8, zero padded)
 void stem_pack_weights(const bf16_t* w, bf16_t* wp, int K, int C, int R, int S, int S2, int KP, hipStream_t st);
 // grad[K,R,S,C] (+)= the stem conv's padded-channel weight gradient (pair form: [K,R,S2,8], else [K,R,S,8])
@@ -260,7 +264,8 @@ void stem_pack_pairs(const bf16_t* x, bf16_t* xp, int N, int H, int W, int C, in
                      hipStream_t st);
 void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
                       const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
-                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st);
+                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st,
+                      const bf16_t* yam = nullptr);
 
 // ---- im2col / col2im, NHWC (im2col.hip) --------------------------------------------------------
 void im2col(const bf16_t* x, bf16_t* cols, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,

@@ -43,7 +43,7 @@ __device__ __forceinline__ float bn_relu_bf(float y, float sc, float sf) {
 template <int KT>
 __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
                                                             bf16_t* __restrict__ out, uint8_t* __restrict__ idx,
-                                                            StemGeom g) {
+                                                            bf16_t* __restrict__ yam, StemGeom g) {
   const unsigned c8n = g.C >> 3;
   const unsigned total = (unsigned)g.N * g.P * g.Q * c8n;  // < 2^31 (host check)
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -54,14 +54,12 @@ __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __rest
     const int p = (int)(t % (unsigned)g.P);
     const int n = (int)(t / (unsigned)g.P);
     float sc[8], sf[8], m[8];
+    uint32_t ym[4] = {0u, 0u, 0u, 0u};  // y at the argmax as raw bf16 pairs (4 VGPRs: the gather's occupancy)
     load8_f32(coef + c8 * 8, sc);
     load8_f32(coef + g.C + c8 * 8, sf);
-    uint8_t am[8];
+    uint32_t am[2] = {0u, 0u};  // window argmax, 4 channels per word
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      m[k] = -INFINITY;
-      am[k] = 0;
-    }
+    for (int k = 0; k < 8; ++k) m[k] = -INFINITY;
     const int h0 = p * g.s - g.pad, w0 = q * g.s - g.pad;
     const bf16_t* yn = y + (long long)n * g.H * g.W * g.C + c8 * 8;
     auto take = [&](const uint4& raw, bool ok, uint8_t wi) {
@@ -72,7 +70,10 @@ __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __rest
         const float a = ok ? bn_relu_bf(v[k], sc[k], sf[k]) : -INFINITY;
         if (a > m[k]) {  // strict: the first maximum in window order wins ties
           m[k] = a;
-          am[k] = wi;
+          am[k >> 2] = (am[k >> 2] & ~(0xffu << (8 * (k & 3)))) | ((uint32_t)wi << (8 * (k & 3)));
+          const uint32_t word = (k >> 1) == 0 ? raw.x : (k >> 1) == 1 ? raw.y : (k >> 1) == 2 ? raw.z : raw.w;
+          ym[k >> 1] = (k & 1) ? ((ym[k >> 1] & 0xffffu) | (word & 0xffff0000u))
+                               : ((ym[k >> 1] & 0xffff0000u) | (word & 0xffffu));
         }
       }
     };
@@ -108,10 +109,8 @@ __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __rest
     }
     const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c8 * 8;
     store8_bf16(out + o, m);
-    uint2 pk;
-    pk.x = am[0] | (am[1] << 8) | (am[2] << 16) | ((uint32_t)am[3] << 24);
-    pk.y = am[4] | (am[5] << 8) | (am[6] << 16) | ((uint32_t)am[7] << 24);
-    *reinterpret_cast<uint2*>(idx + o) = pk;
+    *reinterpret_cast<uint2*>(idx + o) = make_uint2(am[0], am[1]);
+    if (yam) *reinterpret_cast<uint4*>(yam + o) = make_uint4(ym[0], ym[1], ym[2], ym[3]);  // pooled bwd statistics
   }
 }
 
@@ -257,6 +256,82 @@ __global__ void __launch_bounds__(kBlk) stem_bwd_dx_kernel(const bf16_t* __restr
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = fmaf(a[k], dp[k], fmaf(bx[k], yv[k], cc[k]));
     store8_bf16(dy + m * C + c0, o);
+  }
+}
+
+// ---- backward pass 1 at pooled resolution ----------------------------------------------------------------
+// Every pooled gradient lands on exactly one input pixel, its window argmax, and is masked there by
+// relu'(bn(y)).  So sum(dp) = sum over pooled outputs of dout * [bn(y_am) > 0] and sum(dp * xhat) adds
+// dout * [bn(y_am) > 0] * xhat(y_am), y_am = y at the argmax, which the forward pool saved (yam): the same
+// terms as the pixel-resolution pass in another summation order, from the pooled dout + y_am (1/2 of y's
+// bytes at stride 2) instead of y, the pooled dout and the argmax through the window gather.  Each thread
+// keeps one 8-channel chunk (the grid stride is a multiple of C / 8: the host requires 256 % (C / 8) == 0),
+// U chunks' loads in flight per iteration; block-reduced and added into one of kBnStatSlots zeroed slots.
+template <int U>
+__global__ void __launch_bounds__(256) stem_bwd_pooled_stats_kernel(const bf16_t* __restrict__ dout,
+                                                                    const bf16_t* __restrict__ yam,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta,
+                                                                    const float* __restrict__ smean,
+                                                                    const float* __restrict__ sinv, int C,
+                                                                    long long chunks, float* __restrict__ part) {
+  __shared__ float red[2][256][9];
+  const int c8n = C >> 3, c8 = threadIdx.x % c8n, c0 = c8 * 8;
+  float sc[8], sf[8], mu[8], is[8];
+  {
+    float ga[8], be[8];
+    load8_f32(smean + c0, mu);
+    load8_f32(sinv + c0, is);
+    load8_f32(gamma + c0, ga);
+    load8_f32(beta + c0, be);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = ga[k] * is[k];
+      sf[k] = be[k] - mu[k] * sc[k];
+    }
+  }
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto one = [&](const uint4& dr, const uint4& yr) {
+    float d[8], yv[8];
+    gemm::unpack8_bf16(dr, d);
+    gemm::unpack8_bf16(yr, yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dp = fmaf(yv[k], sc[k], sf[k]) > 0.f ? d[k] : 0.f;  // the pixel pass's mask expression
+      s[k] += dp;
+      q[k] += dp * (yv[k] - mu[k]) * is[k];
+    }
+  };
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < chunks; i += U * stride) {
+    uint4 dr[U], yr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dr[u] = *reinterpret_cast<const uint4*>(dout + (i + u * stride) * 8);
+      yr[u] = *reinterpret_cast<const uint4*>(yam + (i + u * stride) * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(dr[u], yr[u]);
+  }
+  for (; i < chunks; i += stride)
+    one(*reinterpret_cast<const uint4*>(dout + i * 8), *reinterpret_cast<const uint4*>(yam + i * 8));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][threadIdx.x][k] = s[k];
+    red[1][threadIdx.x][k] = q[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int cc8 = c >> 3, k = c & 7;
+    float ts = 0.f, tq = 0.f;
+    for (int r = cc8; r < 256; r += c8n) {
+      ts += red[0][r][k];
+      tq += red[1][r][k];
+    }
+    float* slot = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * C;
+    atomicAdd(slot + c, ts);
+    atomicAdd(slot + C + c, tq);
   }
 }
 
@@ -483,14 +558,21 @@ static BnGeom stem_reduce_geom(long long M, int C) {
   return g;
 }
 
+// partial slots of the reduction passes: the gather form's per-chunk partials, at least kBnStatSlots (the
+// banded and pooled passes add into that many zeroed slots)
+static long long stem_part_slots(const BnGeom& g) { return g.nchunk > kBnStatSlots ? g.nchunk : kBnStatSlots; }
+
 long long stem_bwd_workspace_floats(long long M, int C) {
   const BnGeom g = stem_reduce_geom(M, C);
-  return (long long)g.nchunk * 2 * C + 3LL * C;
+  return stem_part_slots(g) * 2 * C + 3LL * C;
 }
+
+bool stem_pooled_stats_ok(int C) { return C % 8 == 0 && C / 8 <= 256 && 256 % (C / 8) == 0; }
 
 void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, const float* beta, float* rmean,
                       float* rvar, float* smean, float* sinv, float* coef, bf16_t* out, uint8_t* idx, int N, int H,
-                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st) {
+                      int W, int C, int k, int s, int pad, int P, int Q, float momentum, float eps, hipStream_t st,
+                      bf16_t* yam) {
   const long long M = (long long)N * H * W;
   bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
                                                          sinv, momentum, eps, coef, nullptr, nullptr, 0); DTG_LAUNCH_CHECK();
@@ -498,39 +580,51 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
   const long long total = (long long)N * P * Q * (C / 8);
   // 3x3 windows (ResNet): the unrolled form with raw-vector loads; other windows: the runtime loop
   if (k == 3)
-    hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, yam, g);
   else
-    hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, g);
+    hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, yam, g);
   DTG_LAUNCH_CHECK();
 }
 
 void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma, const float* beta,
                       const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
-                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st) {
+                      float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st,
+                      const bf16_t* yam) {
   const long long M = (long long)N * H * W;
   const BnGeom bg = stem_reduce_geom(M, C);
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   float* part = ws;
-  float* coef = ws + (long long)bg.nchunk * 2 * C;
-  if (stem_band_ok(H, C, k, s, pad, P, Q) && bg.nchunk >= kBnStatSlots) {
-    const size_t lds = stem_band_lds(Q, C);
-    const unsigned nb = (unsigned)(N * (H / kStemBandRows));
+  float* coef = ws + stem_part_slots(bg) * 2 * C;
+  const bool band = stem_band_ok(H, C, k, s, pad, P, Q) && bg.nchunk >= kBnStatSlots;
+  const size_t lds = stem_band_lds(Q, C);
+  const unsigned nb = (unsigned)(N * (H / kStemBandRows));
+  // pass 1: sum(dp), sum(dp * xhat) -- at pooled resolution when the forward saved y at the argmax, else at
+  // pixel resolution through the window gather (banded for ResNet's geometry)
+  int nslots = kBnStatSlots;
+  if (yam && stem_pooled_stats_ok(C)) {
+    fill_zero(part, (long long)kBnStatSlots * 2 * C * sizeof(float), st);
+    const long long chunks = (long long)N * P * Q * (C / 8);
+    hipLaunchKernelGGL(stem_bwd_pooled_stats_kernel<4>, dim3(grid_for(chunks, 256, 2048)), dim3(256), 0, st, dout,
+                       yam, gamma, beta, smean, sinv, C, chunks, part); DTG_LAUNCH_CHECK();
+  } else if (band) {
     fill_zero(part, (long long)kBnStatSlots * 2 * C * sizeof(float), st);
     hipLaunchKernelGGL(stem_bwd_band_kernel<false>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
                        sinv, nullptr, g, part, nullptr); DTG_LAUNCH_CHECK();
-    bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr,
-                                                           nullptr, nullptr, const_cast<float*>(smean),
-                                                           const_cast<float*>(sinv), 0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
+  } else {
+    dim3 grid(bg.nchunk, bg.gy);
+    DTG_TPR_SWITCH(bg.tpr, stem_bwd_reduce_kernel<T><<<grid, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, g,
+                                                                           M, bg.rows_per_chunk, part)); DTG_LAUNCH_CHECK();
+    nslots = bg.nchunk;
+  }
+  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, nslots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
+                                                         nullptr, const_cast<float*>(smean), const_cast<float*>(sinv),
+                                                         0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
+  // pass 2: dy = a*dp + bx*y + c0
+  if (band) {
     hipLaunchKernelGGL(stem_bwd_band_kernel<true>, dim3(nb), dim3(256), lds, st, dout, idx, y, gamma, beta, smean,
                        sinv, coef, g, nullptr, dy); DTG_LAUNCH_CHECK();
     return;
   }
-  dim3 grid(bg.nchunk, bg.gy);
-  DTG_TPR_SWITCH(bg.tpr, stem_bwd_reduce_kernel<T><<<grid, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, g, M,
-                                                                         bg.rows_per_chunk, part)); DTG_LAUNCH_CHECK();
-  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, bg.nchunk, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
-                                                         nullptr, const_cast<float*>(smean), const_cast<float*>(sinv),
-                                                         0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
   const long long rpa = elementwise_rpc(bg, M);
   dim3 ga((unsigned)((M + rpa - 1) / rpa), bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_dx_kernel<T><<<ga, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, coef, g, M,

@@ -429,6 +429,10 @@ def bottleneck(blk, x):
 # _STEM = False restores conv -> BN -> max-pool as separate ops (A/B tests).
 _STEM = True
 _POOL = (3, 2, 1)  # ResNet's stem max-pool: 3x3, stride 2, pad 1
+# _STEM_YAM = True: the forward pool also saves y at each window's argmax ([N, 56, 56, 64], 1/4 of y), so the
+# backward's BN statistics pass runs over the pooled tensors instead of gathering over y (csrc/kernels/stem.hip
+# stem_bwd_pooled_stats_kernel; exact same terms, another summation order)
+_STEM_YAM = True
 
 
 class _StemFn(torch.autograd.Function):
@@ -450,9 +454,11 @@ class _StemFn(torch.autograd.Function):
             kp = (r * s * 8 + 63) // 64 * 64
             w8 = F.pad(w8, (0, kp - r * s * 8)).contiguous()           # [K, Kp], (r, s, c) columns
             y4, part = L.conv_fwd_c8(x8, w8, r, s, st, pad, True)      # + BN statistics in the epilogue
-        out, idx, smean, sinv = L.stem_bn_pool_fwd(y4, part, gamma, beta, bn.running_mean, bn.running_var,
-                                                   bn.momentum, bn.eps, *_POOL)
-        ctx.save_for_backward(x8, y4, idx, smean, sinv)
+        yam_ok = _STEM_YAM and L.stem_pooled_stats_ok(y4.shape[-1])
+        res = L.stem_bn_pool_fwd(y4, part, gamma, beta, bn.running_mean, bn.running_var, bn.momentum, bn.eps,
+                                 *_POOL, save_yam=yam_ok)
+        out, idx, smean, sinv = res[:4]
+        ctx.save_for_backward(x8, y4, idx, smean, sinv, res[4] if yam_ok else None)
         ctx.stem = stem
         ctx.geom = (c, k, r, s, st, pad)
         return out.permute(0, 3, 1, 2)
@@ -460,13 +466,14 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         L = lib()
-        x8, y4, idx, smean, sinv = ctx.saved_tensors
+        x8, y4, idx, smean, sinv, yam = ctx.saved_tensors
         c, k, r, s, st, pad = ctx.geom
         stem = ctx.stem
         w, gamma, beta = stem.conv.weight, stem.bn.weight, stem.bn.bias
         (dg, dg_direct), (db, db_direct) = _gacc(gamma), _gacc(beta)
         do4 = dout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
-        dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db)[0]
+        dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db,
+                                 yam=yam)[0]
         if ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
             dwp = torch.empty(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)  # beta 0: overwritten
             L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1)

@@ -208,6 +208,36 @@ def test_fused_stem_matches_unfused(flat, pairs, size, monkeypatch):
         assert err < 2e-2, (name, err)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("size", [64, 60])
+def test_stem_pooled_statistics_pass(size, monkeypatch):
+    """The stem backward's BN statistics pass at pooled resolution (the forward saves y at each window's argmax,
+    stem_bwd_pooled_stats_kernel) gives the gradients of the pixel-resolution gather pass up to summation order."""
+    from dtg.models.layers import ConvBN
+    from dtg.models import resnet_fused
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(4, 3, size, size, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for yam in (False, True):
+        monkeypatch.setattr(resnet_fused, "_STEM_YAM", yam)
+        torch.manual_seed(0)
+        stem = ConvBN(3, 64, 7, 2, 3).to(dev)
+        stem.bn.weight.data.uniform_(0.5, 1.5)
+        stem.bn.bias.data.uniform_(-0.3, 0.3)
+        stem.conv.weight.data = stem.conv.weight.data.to(torch.bfloat16)
+        stem.train()
+        xx = x.detach().clone().requires_grad_(False)
+        y = resnet_fused.stem_pool(stem, xx)
+        gy = torch.randn(y.shape, generator=g.manual_seed(7)).to(dev)
+        (y.float() * gy).sum().backward()
+        res.append([t.detach().float().clone() for t in (y, stem.conv.weight.grad, stem.bn.weight.grad,
+                                                          stem.bn.bias.grad)])
+    for name, a, b in zip(["out", "dW", "dgamma", "dbeta"], *res):
+        err = ((a - b).norm() / (a.norm() + 1e-6)).item()
+        assert err < 2e-3, (name, err)
+
+
 def _bf(t):
     """Round to bf16 and back: what dtg stores between kernels."""
     return t.to(torch.bfloat16).to(torch.float32)
