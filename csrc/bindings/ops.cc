@@ -948,7 +948,7 @@ std::tuple<Tensor, c10::optional<Tensor>, Tensor, Tensor> bn_bwd_part(Tensor dp,
 
 // dw (+)= wgrad; dw is [K, R, S, C] contiguous, fp32 or bf16 (beta = 1 accumulates into a flat grad)
 void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int64_t pad, int64_t stride_w,
-                int64_t target_wgs) {
+                int64_t target_wgs, int64_t sched) {
   check_nhwc(dy, "dy");
   check_nhwc(x, "x");
   CHECK_CUDA(dw);
@@ -965,7 +965,7 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
   const int split = dtg::conv_wgrad_split(N, H, W, C, K, R, S, stride, pad, sw, (int)target_wgs);
   auto ws = at::empty({(long long)split * K * R * S * C}, x.options().dtype(at::kFloat));
   dtg::conv_wgrad(cbfp(dy), cbfp(x), dw.data_ptr(), dw.scalar_type() == at::kBFloat16, (float)beta,
-                  ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw);
+                  ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw, (int)sched);
 }
 
 // BN backward in two halves (the BN-folded 1x1 dgrads, models/resnet_fused.py): the finalize of the epilogue
@@ -1035,7 +1035,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("beta") = 0.0, pybind11::arg("zero_rest") = true);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("dw"),
         pybind11::arg("beta"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stride_w") = 0,
-        pybind11::arg("target_wgs") = 0);
+        pybind11::arg("target_wgs") = 0, pybind11::arg("sched") = 0);
   m.def("gemm_bn", &gemm_bn, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("mode"),
         pybind11::arg("x") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("invstd") = pybind11::none(), pybind11::arg("gamma") = pybind11::none(),

@@ -291,6 +291,7 @@ void conv_set_stages(int which, int stages);  // which: 0 fwd, 1 dgrad, 2 wgrad
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w = 0,
                      int target_wgs = 0);  // target 0: 1024 workgroups
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
-                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w = 0);
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w = 0,
+                int sched = 0);  // sched: LDS schedule code of this call (conv_set_stages codes), 0 = default
 
 }  // namespace dtg

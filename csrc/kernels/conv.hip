@@ -618,7 +618,8 @@ int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride
 }
 
 void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, float* ws, int split, int N,
-                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w) {
+                int H, int W, int C, int K, int R, int S, int stride, int pad, hipStream_t st, int stride_w,
+                int sched) {
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   int kps = (M + split - 1) / split;
@@ -631,7 +632,7 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
     dim3 grid(tm * tn, split);
     conv_wgrad_kernel<CF><<<grid, CF::NTH, 0, st>>>(G, dy, x, ws, tn, kps); DTG_LAUNCH_CHECK();
   };
-  const int sc = conv_stages(2);
+  const int sc = sched >= 1 && sched <= 3 && g_conv_stages[2] <= 0 ? sched : conv_stages(2);
   if (K <= 64) run_sched<64, 256>(sc, run);  // 64 output channels: one 64-row tile
   else run_sched<128, 128>(sc, run);
   gemm_splitk_reduce(ws, split, K, No, e, st);

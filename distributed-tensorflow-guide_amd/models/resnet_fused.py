@@ -433,6 +433,11 @@ _POOL = (3, 2, 1)  # ResNet's stem max-pool: 3x3, stride 2, pad 1
 # backward's BN statistics pass runs over the pooled tensors instead of gathering over y (csrc/kernels/stem.hip
 # stem_bwd_pooled_stats_kernel; exact same terms, another summation order)
 _STEM_YAM = True
+# stem weight gradient (pixel-pair form): LDS schedule 3 (register-pipelined) and 512 split-K workgroups, measured
+# 674 vs 748-878 us at b1024 for the default single stage / 1024 (tools/stem_wgrad_ab.py, profiles/r04_stem_pooled);
+# 0 / 0 restore the defaults
+_STEM_WG_SCHED = 3
+_STEM_WG_WGS = 512
 
 
 class _StemFn(torch.autograd.Function):
@@ -476,7 +481,8 @@ class _StemFn(torch.autograd.Function):
                                  yam=yam)[0]
         if ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
             dwp = torch.empty(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)  # beta 0: overwritten
-            L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1)
+            L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1, sched=_STEM_WG_SCHED,
+                         target_wgs=_STEM_WG_WGS)
         else:
             dwp = torch.empty(k, r, s, 8, device=x8.device, dtype=torch.float32)
             L.conv_wgrad(dy4, x8, dwp, 0.0, st, pad)
