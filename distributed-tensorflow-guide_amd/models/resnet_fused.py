@@ -114,8 +114,10 @@ _BITS = True
 # for the 1x1 GEMM wgrads at 128 instead of 512, and +0.7 % for the 3x3 conv wgrads at 512 instead of
 # 1024.  On the main stream (several ranks, or DTG_WGRAD_STREAM=0) the kernels' own defaults stay: there
 # 128 ran 12.4k vs 13.67k img/s (profiles/r02_wgrad_split_policy).  DTG_RESNET_WSPLIT_WGS /
-# DTG_RESNET_CWSPLIT_WGS override the side-stream targets (0: the defaults).
-_WSPLIT_WGS = int(os.environ.get("DTG_RESNET_WSPLIT_WGS", "128"))
+# DTG_RESNET_CWSPLIT_WGS override the side-stream targets (0: the defaults).  Round 4 at b1024, with the stage-1/2
+# conv3 weight gradients fused into the dx passes: 1x1 at 256 beats 128 by 0.3-0.5 % (64: -6 %, 512: +0.1-0.4 %),
+# 3x3 stays at 512 (profiles/r04_wgrad_split).
+_WSPLIT_WGS = int(os.environ.get("DTG_RESNET_WSPLIT_WGS", "256"))
 _CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "512"))
 _wsplit_cache = {}
 
