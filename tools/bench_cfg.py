@@ -4,6 +4,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
 
     DTG_AB_BN_CFG=-1 python tools/bench_cfg.py [bench.py flags]     # BN-epilogue GEMMs without the expand kernel
     DTG_AB_SET=models.resnet_fused._DXW=0 python tools/bench_cfg.py  # a module switch (dtg.<module>.<name>=<int>)
+    DTG_AB_STAGES=0:2,1:3 python tools/bench_cfg.py   # conv LDS schedules per pass (0 fwd, 1 dgrad, 2 wgrad)
 """
 import os
 import runpy
@@ -19,6 +20,9 @@ if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 if os.environ.get("DTG_AB_GEMM_CFG"):
     lib().gemm_force_cfg(int(os.environ["DTG_AB_GEMM_CFG"]))
+for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
+    which, sched = item.split(":")
+    lib().conv_set_stages(int(which), int(sched))
 for item in filter(None, os.environ.get("DTG_AB_SET", "").split(",")):
     path, val = item.split("=")
     mod, name = path.rsplit(".", 1)
