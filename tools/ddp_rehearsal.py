@@ -23,6 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="resnet")
     ap.add_argument("--bucket_mb", type=float, default=2.0)
+    # ResNet: --batch 8 --image 128 reaches the fused dx + weight-gradient passes (stage-1 / 2 rows >= 2048)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--image", type=int, default=64)
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -38,7 +41,7 @@ def main():
     if a.model == "resnet":
         from dtg.models import resnet
         model = resnet.resnet50(num_classes=64).to(device).to(memory_format=torch.channels_last)
-        x, y = resnet.synthetic_batch(4, device, torch.bfloat16, 64, 64, seed=100 + rank)
+        x, y = resnet.synthetic_batch(a.batch, device, torch.bfloat16, a.image, 64, seed=100 + rank)
 
         def loss_fn():
             return ops.softmax_cross_entropy(model(x), y)
