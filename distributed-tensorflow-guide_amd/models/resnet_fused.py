@@ -116,9 +116,9 @@ _BITS = True
 # 128 ran 12.4k vs 13.67k img/s (profiles/r02_wgrad_split_policy).  DTG_RESNET_WSPLIT_WGS /
 # DTG_RESNET_CWSPLIT_WGS override the side-stream targets (0: the defaults).  Round 4 at b1024, with the stage-1/2
 # conv3 weight gradients fused into the dx passes: 1x1 at 256 beats 128 by 0.3-0.5 % (64: -6 %, 512: +0.1-0.4 %),
-# 3x3 stays at 512 (profiles/r04_wgrad_split).
+# and with the 1x1 at 256 the 3x3 at 256 beats 512 by 0.5 % (128: -3 %, 1024: -0.4 %; profiles/r04_wgrad_split).
 _WSPLIT_WGS = int(os.environ.get("DTG_RESNET_WSPLIT_WGS", "256"))
-_CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "512"))
+_CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "256"))
 _wsplit_cache = {}
 
 
