@@ -30,6 +30,22 @@ from ..parallel import grad_sink, overlap
 
 
 _ATTN = "fused"  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax; A/B tests)
+# split-K workgroup target of the weight gradients when they run on the side stream (parallel/overlap.py); 0 = the
+# GEMM's own default (512).  Module switch for the A/B tools (tools/bench_cfg.py DTG_AB_SET).
+_WSPLIT_WGS = 0
+_wsplit_cache = {}
+
+
+def _wgrad(dy, x, out):
+    """out += dy^T x over the token dimension, with the side-stream split target."""
+    tgt = _WSPLIT_WGS if overlap.enabled() else 0
+    sk = 0
+    if tgt > 0:
+        key = (dy.shape[1], x.shape[1], dy.shape[0], tgt)
+        sk = _wsplit_cache.get(key)
+        if sk is None:
+            sk = _wsplit_cache[key] = lib().gemm_pick_split(key[0], key[1], key[2], False, tgt)
+    gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
 
 
 def _fused_attn(S, backward=True):
@@ -101,19 +117,19 @@ class _LayerFn(torch.autograd.Function):
         # LN2: ds2 -> x1 (residual path), df2 -> f2 (dropout branch)
         ds2, df2 = L.ln_bwd(dout, s2, g2, m2, r2, gg2, gbe2, p_h, s_2, 0.0, 0, True, gb_2)  # + db2 = sum(df2)
         with overlap.wgrad_scope(df2, f1):  # weight gradients on the side stream (parallel/overlap.py)
-            gemm(df2, False, f1, False, out=gw_2, beta=1.0)                   # dW2 += df2^T f1
+            _wgrad(df2, f1, gw_2)                   # dW2 += df2^T f1
         dpre = torch.empty_like(pre)
         # df1 * gelu'(pre), and b1's gradient (column sums of it) in the same epilogue
         L.gemm(df2, True, w_2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 4, colsum=gb_1)
         with overlap.wgrad_scope(dpre, x1):
-            gemm(dpre, False, x1, False, out=gw_1, beta=1.0)                  # dW1 += dpre^T x1
+            _wgrad(dpre, x1, gw_1)                  # dW1 += dpre^T x1
         if p_h <= 0:  # df2 aliases ds2: it has been consumed above; accumulate the residual grad into a copy
             ds2 = ds2.clone()
         gemm(dpre, True, w_1, False, out=ds2, beta=1.0)                       # dx1 = dpre W1 + ds2
         # LN1: ds1 -> x (residual), dao -> attention output projection
         ds1, dao = L.ln_bwd(ds2, s1, g1, m1, r1, gg1, gbe1, p_h, s_1, 0.0, 0, True, gb_o)  # + dbo = sum(dao)
         with overlap.wgrad_scope(dao, cx):
-            gemm(dao, False, cx, False, out=gw_o, beta=1.0)
+            _wgrad(dao, cx, gw_o)
         dcx = gemm(dao, True, w_o, False)
         if ctx.fused_attn:
             dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a)
@@ -122,7 +138,7 @@ class _LayerFn(torch.autograd.Function):
             T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
         L.colsum(dqkv, gb_qkv, True)
         with overlap.wgrad_scope(dqkv, x):
-            gemm(dqkv, False, x, False, out=gw_qkv, beta=1.0)
+            _wgrad(dqkv, x, gw_qkv)
         if p_h <= 0:
             ds1 = ds1.clone()
         gemm(dqkv, True, w_qkv, False, out=ds1, beta=1.0)                     # dx = dqkv Wqkv + ds1
