@@ -17,6 +17,7 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 // fp32 zeros on like's device, filled by a dtg kernel on the current stream
 at::Tensor zeros_f32(long long n, const at::Tensor& like) {
+  c10::DeviceGuard dg(like.device());  // the fill runs on like's device's current stream
   at::Tensor t = at::empty({n}, like.options().dtype(at::kFloat));
   dtg::fill_zero(t.data_ptr(), n * 4, cur_stream());
   return t;
@@ -1124,6 +1125,30 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     dtg::stem_dw_add(src.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kBFloat16, K, R, S, C,
                      (int)src.size(2), pair ? 1 : 0, cur_stream());
   });
+  m.def("stream_probe", [](int64_t kind, Tensor a, c10::optional<Tensor> b, c10::optional<Tensor> o, Tensor sink,
+                           int64_t wgs, int64_t unroll, bool nt) {
+    // a / b / o: contiguous GPU buffers of equal byte size (a multiple of 16); sink: int32 [>= wgs]
+    CHECK_IN(a);
+    CHECK_IN(sink);
+    TORCH_CHECK(sink.scalar_type() == at::kInt && sink.numel() >= wgs, "sink: int32 with >= wgs elements");
+    const long long bytes = a.numel() * a.element_size();
+    TORCH_CHECK(bytes % 16 == 0 && ((uintptr_t)a.data_ptr() % 16) == 0, "a: 16-B multiple, 16-B aligned");
+    for (const auto* t : {&b, &o})
+      if (t->has_value() && (*t)->defined()) {
+        CHECK_IN(**t);
+        TORCH_CHECK((*t)->numel() * (*t)->element_size() == bytes && ((uintptr_t)(*t)->data_ptr() % 16) == 0,
+                    "b / o: the byte size of a, 16-B aligned");
+      }
+    TORCH_CHECK(kind >= 0 && kind <= 3, "kind 0..3");
+    TORCH_CHECK(kind == 0 || (o.has_value() && o->defined()), "kinds 1-3 write o");
+    TORCH_CHECK(kind != 3 || (b.has_value() && b->defined()), "kind 3 reads b");
+    TORCH_CHECK(wgs >= 1 && wgs <= 65536, "wgs");
+    c10::DeviceGuard dg(a.device());
+    dtg::stream_probe((int)kind, a.data_ptr(), opt_ptr<void>(b), opt_ptr<void>(o), bytes / 16,
+                      reinterpret_cast<unsigned*>(sink.data_ptr()), (int)wgs, (int)unroll, nt ? 1 : 0, cur_stream());
+  }, pybind11::arg("kind"), pybind11::arg("a"), pybind11::arg("b") = pybind11::none(),
+        pybind11::arg("o") = pybind11::none(), pybind11::arg("sink"), pybind11::arg("wgs") = 1024,
+        pybind11::arg("unroll") = 4, pybind11::arg("nt") = false);
   m.def("launch_probe", [](int64_t grid, int64_t lds_bytes) {
     dtg::launch_probe((int)grid, (int)lds_bytes, cur_stream());
   });

@@ -32,6 +32,9 @@ void fill_zero(void* p, long long bytes, hipStream_t st);
 // ---- emulated blocking collective (comm_emu.hip; parallel/ddp.py DTG_COMM_EMULATE) ------------------
 void comm_spin(double seconds, int wgs, int lds_bytes, hipStream_t st);
 void launch_probe(int grid, int lds_bytes, hipStream_t st);
+// HBM streaming probe (stream_probe.hip): kind 0 read, 1 write, 2 copy, 3 read2/write1 over n16 16-B vectors
+void stream_probe(int kind, const void* a, const void* b, void* o, long long n16, unsigned* sink, int wgs, int unroll,
+                  int nt, hipStream_t st);
 
 // ---- BatchNorm statistics fused into a GEMM / implicit-GEMM epilogue (dtg/bn_epi.cuh) ----------
 // mode 1 (forward): per output column c, sum and sum of squares of the stored (bf16) output.

@@ -203,7 +203,9 @@ int dx_wgrad_grid() {
     DTG_HIP_CHECK(hipGetDevice(&dev));
     DTG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     DTG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bn_dx_wgrad_kernel<CI, true, W2>, 256, 0));
-    G = cus * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));  // a multiple of 8 and of the slice count (<= 2)
+    G = cus * (per_cu < 1 ? 1 : (per_cu > 2 ? 2 : per_cu));
+    G -= G % 8;  // a multiple of 8 (the XCD count) and so of the slice count (<= 2) on any CU count
+    if (G < 8) G = 8;
   }
   return G;
 }

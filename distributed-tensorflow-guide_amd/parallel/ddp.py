@@ -67,7 +67,12 @@ class DataParallel:
         self._force = forced
         self._comm = True  # set_comm(False): gradients stay rank-local (bench.py's compute-only timing)
         self._estreams = {}
-        self.emulate = EMULATE if self.overlap else None
+        # the emulated collective stands in for peers a one-rank run does not have: with real peers it would
+        # add spin kernels on top of the real collectives and skew the scaling numbers, so it is refused there
+        if EMULATE is not None and self.world > 1:
+            import warnings
+            warnings.warn("DTG_COMM_EMULATE is ignored at world size %d (one-rank rehearsals only)" % self.world)
+        self.emulate = EMULATE if (self.overlap and self.world == 1) else None
         self.buckets = []
         self._hooks = []
         cap = int(bucket_mb * (1 << 20))

@@ -33,8 +33,9 @@ def main():
         c = a + b
         target = dtg.constant(100., shape=[2], dtype=dtg.float32)
         loss = dtg.reduce_mean(dtg.square(c - target))
-        global_step = dtg.train.get_or_create_global_step()
-        opt = dtg.train.GradientDescentOptimizer(.0001).minimize(loss, global_step=global_step)
+        # no global step, as in the reference (minimize(loss) only): the Supervisor's checkpoints are plain
+        # `model.ckpt` files holding just Variable and Variable_1
+        opt = dtg.train.GradientDescentOptimizer(.0001).minimize(loss)
 
     logdir = FLAGS.logdir or os.path.join(os.getcwd(), 'logdir')
     sv = dtg.train.Supervisor(logdir=logdir, is_chief=is_chief, save_model_secs=30)

@@ -128,10 +128,15 @@ def test_hogwild_two_workers(tmp_path):
     assert all(b <= a + 1e-3 for a, b in zip(gaps, gaps[1:]))  # monotone toward 100
     import dtg
     ck = dtg.train.latest_checkpoint(str(tmp_path / "l"))
+    # the reference minimises without a global step (Hogwild/Hogwild.py:44), so its Supervisor writes a plain
+    # model.ckpt holding only the two variables
+    assert os.path.basename(ck) == "model.ckpt", ck
     r = dtg.train.NewCheckpointReader(ck)
-    # the chief's final save happens when IT finishes: its 300 applies are in, the other worker's
-    # are in flight (the PS counts every lock-free apply exactly once under the step lock)
-    assert 300 <= int(r.get_tensor("global_step")) <= 600
+    assert set(r.get_variable_to_shape_map()) == {"Variable", "Variable_1"}
+    # the chief's final save holds its own 300 applies and whatever of the other worker's had landed: c moved
+    # from ~0 most of the way a 300-step run gets toward 100
+    c = r.get_tensor("Variable") + r.get_tensor("Variable_1")
+    assert all(100 - v <= gaps[-1] + 1e-3 for v in c)
 
 
 def test_distributed_setup_mts():
@@ -149,6 +154,10 @@ def test_multi_gpu_example_runs_on_cpu(tmp_path):
     out = run_cluster("Multiple-GPUs-Single-Machine/dist_mult_gpu_sing_mach.py", 1, 2,
                       ["--steps", "40", "--logdir", str(tmp_path / "l")], env={"HIP_VISIBLE_DEVICES": "-1"})
     _ok(out)
+    import dtg
+    ck = dtg.train.latest_checkpoint(str(tmp_path / "l"))  # no global step in the reference either
+    assert os.path.basename(ck) == "model.ckpt", ck
+    assert set(dtg.train.NewCheckpointReader(ck).get_variable_to_shape_map()) == {"Variable", "Variable_1"}
 
 
 def test_non_distributed_gap_factor():
