@@ -37,6 +37,18 @@ MI355X design:
   request from any live worker (TimeoutError naming them).  A worker that dies in the middle of a
   transfer leaves an RCCL kernel waiting on its pair stream; RCCL communicators cannot shrink, so that
   case is fail-stop (the other workers' pulls stall and the PS times out), like sync DP.
+* **GPU-ready request order**: a worker's host enqueues a step long before its GPU has the gradient.  Its
+  request token therefore goes out from a small announcer thread only once a device event recorded after the
+  gradient has completed (:class:`_Announcer`), so the PS -- which posts the receive and makes its apply stream
+  wait for it as soon as it dequeues a token -- serves workers in the order their gradients EXIST, never
+  stalls its apply stream behind a worker that is still in backward, and fast workers take proportionally
+  more updates than a slow one (``test_async_ps_slow_worker_does_not_hold_back_fast_ones``).  The PS also
+  bounds how many requests' device work it has queued (``max_inflight``; the host waits on the oldest
+  request's completion event beyond it), so its pair streams cannot pile up.
+* **staleness** tau of an update = the number of PS updates applied between the pushing worker's last pull
+  (the parameter snapshot its gradient was computed on) and this update.  With W workers in round-robin tau is
+  about W - 1; ``overlap_pull`` adds one exchange (about W more): the one-card 1 PS + 7 worker rehearsal with
+  overlapped pulls measured a mean of 6.0 (``profiles/r04_async_ps``).
 * **overlap** (``overlap_pull=True``): the worker snapshots its gradients into a send buffer, posts the
   push and the pull, and goes on with its next step on the parameters it already has; the pulled ones
   are swapped in (a device copy) at its next exchange.  That adds one step of staleness, which Hogwild
@@ -174,6 +186,59 @@ class _Control:
             self.svc = None
 
 
+class _Announcer:
+    """Sends a worker's request tokens from a background thread, each only after the device event it carries
+    has completed (None: at once), in submission order.  The worker's host thread never blocks on its own GPU
+    for this, and the PS sees a gradient's token only when the gradient is on the device."""
+
+    def __init__(self, ctl):
+        import queue
+        import threading
+        self._ctl = ctl
+        self._q = queue.Queue()
+        self.error = None
+        self._t = threading.Thread(target=self._run, name="dtg-aps-announce", daemon=True)
+        self._t.start()
+
+    def _run(self):
+        while True:
+            item = self._q.get()
+            if item is None:
+                return
+            rank, kind, ev = item
+            try:
+                if ev is not None:
+                    ev.synchronize()
+                self._ctl.request(rank, kind)
+            except Exception as e:  # surfaced by the next submit()/close()
+                self.error = e
+                return
+
+    def _check(self):
+        if self.error is not None:
+            raise RuntimeError("async PS request announcer failed") from self.error
+
+    def submit(self, rank, kind, event=None):
+        self._check()
+        self._q.put((rank, kind, event))
+
+    def close(self):
+        """Flush every queued token (in order) and stop the thread."""
+        self._q.put(None)
+        self._t.join()
+        self._check()
+
+
+def _ready_event(tensors):
+    """A device event after the work that produces ``tensors`` (None for host tensors)."""
+    t = next((t for t in tensors if t.is_cuda), None)
+    if t is None:
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+
 class AsyncPSWorker:
     """Worker side.  ``begin()`` pulls the current parameters, ``step_done()`` after every backward
     pushes/pulls every ``window`` steps, ``warm()`` marks the end of a warm-up phase (benchmarks),
@@ -191,6 +256,7 @@ class AsyncPSWorker:
         self.local_opt = local_optimizer
         self.overlap = bool(overlap_pull)
         self._ctl = _Control(False, self.rank)
+        self._ann = _Announcer(self._ctl)
         self._acc = [torch.zeros_like(g.grad) for g in flat] if (self.window > 1 and local_optimizer) else None
         # module buffers as pulled: the push carries (current - pulled), the worker's running-statistics
         # update since the pull, which the PS adds to its own copy
@@ -253,7 +319,8 @@ class AsyncPSWorker:
             grads_out = self._gsnap
         else:
             grads_out = grads
-        self._ctl.request(self.rank, _GRAD)
+        # the token goes out when the gradient exists on the device (announcer thread), the sends are posted now
+        self._ann.submit(self.rank, _GRAD, _ready_event(list(grads_out) + self._bufd))
         self._sends = [_isend(t, self.ps, self.pg) for t in list(grads_out) + self._bufd]
         if self.overlap:
             self._pull = [_irecv(t, self.ps, self.pg) for t in self._pbuf]
@@ -272,12 +339,13 @@ class AsyncPSWorker:
 
     def warm(self):
         """Tell the PS this worker has finished its warm-up (``AsyncPSServer.timed`` starts when all have)."""
-        self._ctl.request(self.rank, _WARM)
+        self._ann.submit(self.rank, _WARM)
 
     def finish(self):
         self._land_pull()
         _wait_all(self._sends)
         self._sends = []
+        self._ann.close()  # every GRAD / WARM token is out before DONE
         self._ctl.unwatch()
         self._ctl.request(self.rank, _DONE)
         self._ctl.close()
@@ -287,7 +355,7 @@ class AsyncPSServer:
     """PS side: ``serve()`` runs until every worker sent DONE (or was lost); returns the number of updates."""
 
     def __init__(self, flat, optimizer, workers, window=1, window_mode="sum", group=None, staleness_log=False,
-                 staleness_scaling=None, worker_timeout=None):
+                 staleness_scaling=None, worker_timeout=None, max_inflight=None):
         assert staleness_scaling in (None, "dyn")
         self.dyn = staleness_scaling == "dyn"
         self.flat = flat
@@ -313,6 +381,14 @@ class AsyncPSServer:
         self.lost = []
         self._warm = set()
         self.timed = None  # (updates, time) when every worker reported warm; serve() fills timed_end
+        # applied order: (worker, that worker's push index) per update -- what a replay of the PS must follow
+        self.order = []
+        self._push_idx = {w: 0 for w in self.workers}
+        # requests whose device work (receive, apply, snapshot, send) may be queued at once; beyond that the host
+        # waits for the oldest one's completion event (one outstanding request per worker by default)
+        self.max_inflight = int(max_inflight if max_inflight is not None else
+                                os.environ.get("DTG_PS_MAX_INFLIGHT", str(max(1, len(self.workers)))))
+        self._inflight = []
 
     def _send_params(self, w):
         _wait_all(self._send_works[w])  # the snapshot buffer is about to be overwritten (stream wait)
@@ -345,13 +421,28 @@ class AsyncPSServer:
         self.version += 1
         self.updates += 1
         self.per_worker[w] += 1
+        self.order.append((w, self._push_idx[w]))
+        self._push_idx[w] += 1
+
+    def _bound_inflight(self):
+        """Record this request's completion on the apply stream; wait for the oldest beyond max_inflight."""
+        if self.dev.type != "cuda":
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self._inflight.append(ev)
+        while len(self._inflight) > self.max_inflight:
+            self._inflight.pop(0).synchronize()
 
     def _grad(self, w):
         # the receive is posted from the apply (current) stream, so RCCL's pair stream first waits for the
-        # previous apply that read these buffers; the apply then waits for the receive (stream events only)
+        # previous apply that read these buffers; the apply then waits for the receive (stream events only).
+        # The worker sent this token only once its gradient was on its device (_Announcer), so the receive
+        # completes as soon as the pair's transfer does.
         _wait_all([_irecv(b, w, self.pg) for b in self._recv[w] + self._recv_buf[w]])
         self._apply(w)
         self._send_params(w)
+        self._bound_inflight()
 
     def _elastic(self, w):
         """EASGD exchange (Zhang, Choromanska, LeCun 2015): receive the worker's parameters x_i,

@@ -285,10 +285,12 @@ def test_async_ps_carries_bn_running_stats():
 
 
 def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeout=None, stall=None, env=None,
-               step_sleep=0.0):
+               step_sleep=0.0, duration=None, slow=None):
     """Hogwild ranks with the worker-side options: overlapped pulls, a worker that dies (os._exit, no
     finish) after ``die_after`` steps, a PS ``worker_timeout`` with a worker that stalls; ``env`` extra
-    environment (e.g. a short rank-liveness timeout), ``step_sleep`` seconds per worker step."""
+    environment (e.g. a short rank-liveness timeout), ``step_sleep`` seconds per worker step; ``duration``: the
+    workers step until that many seconds have passed (``steps`` ignored); ``slow`` = (rank, seconds): that
+    worker takes that much longer to produce each gradient."""
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -319,9 +321,13 @@ def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeo
             w = AsyncPSWorker(flat, ps_rank=0, overlap_pull=overlap)
             w.begin()
             x, y = _data(rank)
-            for i in range(steps):
+            t_end = time.time() + duration if duration else None
+            i = 0
+            while (i < steps) if t_end is None else (time.time() < t_end):
                 loss = ops.softmax_cross_entropy(model(x), y)
                 loss.backward()
+                if slow is not None and rank == slow[0]:
+                    time.sleep(slow[1])  # a slow worker: its gradient takes this much longer to exist
                 w.step_done()
                 if step_sleep:
                     time.sleep(step_sleep)
@@ -336,6 +342,7 @@ def _rank_opts(rank, world, port, steps, q, overlap=False, die_after=None, timeo
                     q.join_thread()
                     time.sleep(60)
                     os._exit(0)
+                i += 1
             w.finish()
             q.put((rank, "ok", {"pushes": w.pushes}))
         comm.shutdown()
@@ -432,3 +439,50 @@ def test_async_ps_one_ps_seven_workers(overlap):
 def test_async_ps_worker_timeout_names_silent_workers():
     out = _run_opts(2, 6, timeout=3.0, stall=2)
     assert "no request from workers [1]" in out[0]["timeout"]
+
+
+def test_async_ps_slow_worker_does_not_hold_back_fast_ones():
+    """1 PS + 3 workers for 4 s, worker 3 taking 0.25 s longer per gradient: the PS serves gradients in the
+    order they exist, so the two fast workers take proportionally more updates instead of waiting for it
+    (Hogwild semantics, /root/reference/Hogwild/Hogwild.py:44-57), and every push is applied once."""
+    out = _run_opts(4, 0, duration=4.0, slow=(3, 0.25))
+    ps = out[0]
+    assert ps["lost"] == []
+    pw = ps["per_worker"]
+    assert pw[3] <= 17, pw
+    assert min(pw[1], pw[2]) >= 4 * pw[3], pw
+    assert sum(out[r]["pushes"] for r in (1, 2, 3)) == ps["updates"]
+
+
+def test_announcer_sends_tokens_only_after_their_events_in_order():
+    """The worker-side announcer (parallel/async_ps.py::_Announcer): submit() returns at once, each token is
+    sent only after its event completes, and tokens keep their submission order."""
+    import threading
+    import time
+    import dtg  # noqa: F401
+    from dtg.parallel.async_ps import _Announcer
+
+    class Ev:
+        def __init__(self, delay):
+            self.delay, self.done = delay, threading.Event()
+
+        def synchronize(self):
+            time.sleep(self.delay)
+            self.done.set()
+
+    sent = []
+
+    class Ctl:
+        def request(self, rank, kind):
+            sent.append((rank, kind, time.perf_counter()))
+
+    a = _Announcer(Ctl())
+    e1, e2 = Ev(0.3), Ev(0.0)
+    t0 = time.perf_counter()
+    a.submit(1, 1, e1)
+    a.submit(1, 4, e2)
+    a.submit(1, 2)
+    assert time.perf_counter() - t0 < 0.1  # the host never waits for the device here
+    a.close()
+    assert [k for _, k, _ in sent] == [1, 4, 2]
+    assert sent[0][2] - t0 >= 0.3 and e1.done.is_set()

@@ -36,3 +36,51 @@ def test_bench_async_ps_mode_one_card():
     assert len(rows) == 1
     j = rows[0]
     assert j["n_gpus"] == 2 and j["dtype"] == "bf16" and j["per_worker"] == {"1": 6} and j["value"] > 0
+
+
+@pytest.mark.gpu
+def test_async_ps_token_waits_for_device_gradient():
+    """The worker's request token leaves only when its gradient exists on the device: an event recorded behind
+    a 0.2 s device spin (comm_spin stands in for a slow backward) holds the token back 0.2 s, while the host
+    that submitted it returned at once (parallel/async_ps.py::_Announcer, _ready_event)."""
+    import time
+
+    import torch
+    from dtg.ops import lib
+    from dtg.parallel.async_ps import _Announcer, _ready_event
+
+    sent = []
+
+    class Ctl:
+        def request(self, rank, kind):
+            torch.cuda.current_stream()  # (touches nothing on the device)
+            sent.append((rank, kind, time.perf_counter()))
+
+    g = torch.zeros(1 << 20, device="cuda", dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    a = _Announcer(Ctl())
+    t0 = time.perf_counter()
+    lib().comm_spin(0.2, 1, 0)  # the "backward" producing g is still running ...
+    g.add_(1.0)
+    a.submit(3, 1, _ready_event([g]))
+    t_submit = time.perf_counter() - t0
+    a.close()
+    assert t_submit < 0.1, t_submit
+    assert sent and sent[0][:2] == (3, 1)
+    assert sent[0][2] - t0 >= 0.19, sent[0][2] - t0
+    assert g.float().mean().item() == 1.0
+
+
+@pytest.mark.gpu
+def test_async_ps_slow_worker_one_card():
+    """1 PS + 3 workers on one card (gloo, device tensors staged through the host), worker 3's gradients
+    delayed by a device spin before each push: the fast workers take proportionally more updates."""
+    import json
+    env = dict(os.environ, DTG_BACKEND="gloo", DTG_GLOO_DEVICE="cuda", DTG_APS_TEST_SLOW="3:0.2")
+    r = subprocess.run(["python", os.path.join(ROOT, "tools", "async_ps_slow_worker.py"), "--workers", "3",
+                        "--seconds", "6"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    pw = {int(k): v for k, v in rows[-1]["per_worker"].items()}
+    assert rows[-1]["lost"] == [] and pw[3] >= 1, pw
+    assert min(pw[1], pw[2]) >= 3 * pw[3], pw

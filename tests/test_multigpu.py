@@ -16,12 +16,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(n, env, timeout=600):
+def _run(n, env, timeout=600, names=()):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _cluster import free_ports
     port = free_ports(1)[0]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n), "--master-addr",
-           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "multigpu_checks.py")]
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "multigpu_checks.py"), *names]
     e = dict(os.environ, OMP_NUM_THREADS="2")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         e.pop(k, None)
@@ -30,14 +30,23 @@ def _run(n, env, timeout=600):
     rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert r.returncode == 0 and rows and rows[0]["ok"], (r.stdout + r.stderr)[-4000:]
     j = rows[0]
-    assert j["world"] == n and set(j["checks"]) == {"allreduce", "dp_resnet", "dp_bert", "async_ps"}
-    assert j["checks"]["async_ps"]["updates"] == 5 * (n - 1)
+    assert j["world"] == n and set(j["checks"]) == (set(names) or {"allreduce", "dp_resnet", "dp_bert", "async_ps"})
+    if "async_ps" in j["checks"]:
+        assert j["checks"]["async_ps"]["updates"] == 5 * (n - 1)
+        assert j["checks"]["async_ps"]["replay_max_rel_err"] < 1e-5  # PS state == replay in its logged order
     return j
 
 
 def test_multirank_checks_cpu_gloo():
     j = _run(2, {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
     assert j["backend"] == "gloo" and j["device"] == "cpu"
+
+
+def test_async_ps_replay_three_ranks_cpu():
+    """1 PS + 2 workers (one with overlapped pulls): the PS parameters equal the replay of both workers'
+    pushes in the order the PS applied them."""
+    j = _run(3, {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}, names=("async_ps",))
+    assert sorted({w for w, _ in j["checks"]["async_ps"]["order_head"]}) == [1, 2]
 
 
 @pytest.mark.gpu

@@ -7,7 +7,8 @@
                 give the mean of the N per-shard gradients, computed here on one process shard by shard;
 * dp_bert    -- DataParallel over a 2-layer BERT (dropout off): N ranks x B equals ONE process on the
                 full N*B batch;
-* async_ps   -- 1 PS + (N-1) workers: every pushed gradient is applied exactly once.
+* async_ps   -- 1 PS + (N-1) workers: every pushed gradient is applied exactly once, and the PS parameters
+                equal a replay of the pushed gradients in the PS's logged order.
 
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/multigpu_checks.py
     (RCCL, one GPU per rank; DTG_BACKEND=gloo DTG_GLOO_DEVICE=cuda rehearses it with N ranks on one card)
@@ -109,29 +110,46 @@ def check_dp_bert(rank, world, device, B=4, S=64):
 
 
 def check_async_ps(rank, world, device, steps=5):
+    """1 PS + (N-1) workers: every push applied once, AND the PS parameters equal a replay of the pushed
+    gradients in the order the PS logged (AsyncPSServer.order): each worker records what it pushed and
+    sends it to the PS after the run, the PS re-applies them to its initial parameters with the same SGD."""
     from dtg.models.layers import Linear
     from dtg.optim import FusedSGD
-    from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
+    from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker, _irecv, _isend, _wait_all
     torch.manual_seed(0)
     model = torch.nn.Sequential(Linear(64, 128, act="relu"), Linear(128, 10)).to(device)
     dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
     flat = FlatParams(model, compute_dtype=dtype)
+    lr = 0.05
     if rank == 0:
-        ps = AsyncPSServer(flat, FusedSGD(flat, lr=0.05, momentum=0.0), workers=range(1, world))
+        init = [g.master.clone() for g in flat]
+        ps = AsyncPSServer(flat, FusedSGD(flat, lr=lr, momentum=0.0), workers=range(1, world))
         n = ps.serve()
         ps.close()
         expect = {w: steps for w in range(1, world)}
         assert n == steps * (world - 1) and ps.per_worker == expect and not ps.lost, (n, ps.per_worker, ps.lost)
-        return {"updates": n}
+        pushed = {w: [[torch.empty_like(g.grad) for g in flat] for _ in range(steps)] for w in range(1, world)}
+        _wait_all([_irecv(t, w, None) for w in pushed for gs in pushed[w] for t in gs])
+        rep = [m.clone() for m in init]
+        for w, i in ps.order:  # the PS's applied order
+            for m, gr in zip(rep, pushed[w][i]):
+                m.sub_(lr * gr.float())
+        err = max(((m - r).abs().max() / (r.abs().max() + 1e-12)).item() for m, r in
+                  zip([g.master for g in flat], rep))
+        assert err < 1e-5, err
+        return {"updates": n, "replay_max_rel_err": err, "order_head": ps.order[:8]}
     w = AsyncPSWorker(flat, ps_rank=0, overlap_pull=rank % 2 == 0)
     g = torch.Generator().manual_seed(rank)
     x = torch.randn(32, 64, generator=g).to(device, dtype)
     y = torch.randint(0, 10, (32,), generator=g).to(device)
     w.begin()
+    pushed = []
     for _ in range(steps):
         ops.softmax_cross_entropy(model(x), y).backward()
+        pushed.append([gr.grad.clone() for gr in flat])  # what step_done pushes (window 1)
         w.step_done()
     w.finish()
+    _wait_all([_isend(t, 0, None) for gs in pushed for t in gs])
     return {"pushes": w.pushes}
 
 
