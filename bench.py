@@ -195,6 +195,17 @@ def main(argv=None):
     if use_graph:
         # warmup = eager steps on a side stream + the capture; the rest of the warmup replays
         step = GraphedStep(step, warmup=min(2, max(a.warmup - 1, 1)))
+    main_prio = os.environ.get("DTG_MAIN_PRIO")
+    if main_prio is not None and device.type == "cuda" and not use_graph:
+        # the whole step on a stream of this priority (A/B of the main / side stream priorities, DTG_SIDE_PRIO)
+        ms = torch.cuda.Stream(device=device, priority=int(main_prio))
+        ms.wait_stream(torch.cuda.current_stream(device))
+        step0 = step
+
+        def step():
+            with torch.cuda.stream(ms):
+                return step0()
+        print(f"main stream priority {int(main_prio)}, range {torch.cuda.Stream.priority_range()}", file=sys.stderr)
     for _ in range(a.warmup):
         loss = step()
     sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)

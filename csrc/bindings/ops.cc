@@ -493,25 +493,14 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
                                    c10::optional<Tensor> mask, c10::optional<Tensor> out, bool pooled,
                                    c10::optional<Tensor> x2, c10::optional<Tensor> mean2,
                                    c10::optional<Tensor> invstd2, c10::optional<Tensor> part2,
-                                   c10::optional<std::tuple<int64_t, int64_t>> sub2_hw,
-                                   c10::optional<Tensor> xcoef, c10::optional<Tensor> a2,
-                                   c10::optional<Tensor> colbias) {
+                                   c10::optional<std::tuple<int64_t, int64_t>> sub2_hw) {
   CHECK_IN(A);
   CHECK_DT(A, at::kBFloat16);
   CHECK_CUDA(B);
   CHECK_DT(B, at::kBFloat16);
   TORCH_CHECK(mode >= 1 && mode <= 3, "mode in {1, 2, 3}");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && B.stride(1) == 1, "2-D operands, contiguous rows");
-  const bool two = a2.has_value() && a2->defined();
-  const int M = (int)A.size(0), K = (int)A.size(1) + (two ? (int)a2->size(1) : 0);
-  if (two) {  // BN-folded dgrad: A operand = [A | a2] along K (BnEpi::a2)
-    TORCH_CHECK(mode == 3, "a2 (K-concatenated A) is mode 3 only");
-    CHECK_IN(*a2);
-    CHECK_DT(*a2, at::kBFloat16);
-    TORCH_CHECK(a2->dim() == 2 && a2->size(0) == M && A.size(1) % 64 == 0 && a2->size(1) % 8 == 0,
-                "a2 must be [M, K2] with the first part's K a multiple of 64");
-    TORCH_CHECK(((uintptr_t)a2->data_ptr() % 16) == 0 && a2->stride(0) % 8 == 0, "a2: 16-byte aligned rows");
-  }
+  const int M = (int)A.size(0), K = (int)A.size(1);
   const int N = (int)(mode == 1 ? B.size(0) : B.size(1));
   TORCH_CHECK((mode == 1 ? B.size(1) : B.size(0)) == K, "gemm_bn K mismatch");
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0 && B.stride(0) % 8 == 0, "K, N and row strides must be multiples of 8");
@@ -573,109 +562,9 @@ std::tuple<Tensor, Tensor> gemm_bn(Tensor A, Tensor B, int64_t mode, c10::option
   } else {
     bn.part = part.data_ptr<float>();
     bn.mode = 1;
-    if (xcoef.has_value() && xcoef->defined()) {  // A is the previous BN's input: its apply + relu in the prologue
-      CHECK_IN(*xcoef);
-      CHECK_DT(*xcoef, at::kFloat);
-      TORCH_CHECK(xcoef->numel() == 2LL * K, "xcoef must hold scale[K] and shift[K]");
-      TORCH_CHECK(((uintptr_t)xcoef->data_ptr() % 16) == 0 && K % 8 == 0, "xcoef must be 16-byte aligned");
-      bn.xcoef = xcoef->data_ptr<float>();
-      bn.xc_n = K;
-    }
-  }
-  if (two) {
-    bn.a2 = cbfp(*a2);
-    bn.lda2 = a2->stride(0);
-    bn.ka1 = (int)A.size(1);
-  }
-  if (colbias.has_value() && colbias->defined()) {
-    TORCH_CHECK(mode == 3, "colbias is mode 3 only");
-    CHECK_IN(*colbias);
-    CHECK_DT(*colbias, at::kFloat);
-    TORCH_CHECK(colbias->numel() == N && ((uintptr_t)colbias->data_ptr() % 16) == 0, "colbias must be [N] fp32");
-    bn.colbias = colbias->data_ptr<float>();
   }
   dtg::gemm_bf16_bn(cbfp(A), A.stride(0), cbfp(B), B.stride(0), bfp(o), N, M, N, K, bt, bn, cur_stream());
   return {o, part};
-}
-
-// experimental: direct 3x3 conv (C = K = 64, stride 1, pad 1) from an LDS halo tile (csrc/kernels/conv_halo.hip)
-Tensor conv_halo_fwd(Tensor x, Tensor w) {
-  check_nhwc(x, "x");
-  check_nhwc(w, "w");
-  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C, "w must be [64, 3, 3, C]");
-  TORCH_CHECK(dtg::conv3x3_halo_supported(C, (int)w.size(0), H, W), "conv_halo_fwd: C = K = 64, H % 4 == 0, W <= 64");
-  c10::DeviceGuard dg(x.device());
-  auto y = at::empty({N, H, W, 64}, x.options());
-  dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream());
-  return y;
-}
-
-// the same with the BatchNorm forward statistics of the output: (y, part) as conv_fwd_bn returns them
-std::tuple<Tensor, Tensor> conv_halo_fwd_bn(Tensor x, Tensor w) {
-  check_nhwc(x, "x");
-  check_nhwc(w, "w");
-  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 && w.size(3) == C, "w must be [64, 3, 3, C]");
-  TORCH_CHECK(dtg::conv3x3_halo_supported(C, 64, H, W, 1), "conv_halo_fwd_bn: C = K = 64, H % 4 == 0, W <= 56");
-  c10::DeviceGuard dg(x.device());
-  auto y = at::empty({N, H, W, 64}, x.options());
-  auto part = bn_part(x, 64, false);
-  dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream(), part.data_ptr<float>());
-  return {y, part};
-}
-
-// BN statistics from epilogue partials without the apply pass -> (mean, invstd, coef = [scale[C], shift[C]]);
-// the consumer GEMM applies relu(x * scale + shift) to its operand (gemm_bn xcoef / gemm_xb)
-std::tuple<Tensor, Tensor, Tensor> bn_finalize(Tensor part, Tensor gamma, Tensor beta, Tensor rmean, Tensor rvar,
-                                               int64_t M, double momentum, double eps) {
-  CHECK_IN(part);
-  CHECK_DT(part, at::kFloat);
-  const int C = (int)gamma.numel();
-  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
-  for (const Tensor* t : {&gamma, &beta, &rmean, &rvar}) {
-    CHECK_IN(*t);
-    CHECK_DT(*t, at::kFloat);
-    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
-  }
-  c10::DeviceGuard dg(part.device());
-  auto fopt = part.options();
-  auto smean = at::empty({C}, fopt), sinv = at::empty({C}, fopt), coef = at::empty({2LL * C}, fopt);
-  dtg::bn_finalize_part(part.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
-                        rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(),
-                        sinv.data_ptr<float>(), coef.data_ptr<float>(), M, C, (float)momentum, (float)eps,
-                        cur_stream());
-  return {smean, sinv, coef};
-}
-
-// out[M,N] (+)= A^T relu(B * coef[n] + coef[N + n]) for A [K,M], B [K,N] (both MN-contiguous): the weight
-// gradient of a 1x1 conv whose input is a BN + ReLU output, read from the BN's raw input B
-void gemm_xb(Tensor A, Tensor B, Tensor out, Tensor coef, double beta, int64_t split_k) {
-  CHECK_IN(A);
-  CHECK_IN(B);
-  CHECK_IN(out);
-  CHECK_IN(coef);
-  CHECK_DT(A, at::kBFloat16);
-  CHECK_DT(B, at::kBFloat16);
-  CHECK_DT(coef, at::kFloat);
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && out.dim() == 2 && A.size(0) == B.size(0), "A [K,M], B [K,N]");
-  const int K = (int)A.size(0), M = (int)A.size(1), N = (int)B.size(1);
-  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "out must be a contiguous [M, N]");
-  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "out fp32/bf16");
-  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "16-byte rows");
-  TORCH_CHECK(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0, "16-byte alignment");
-  TORCH_CHECK(coef.numel() == 2LL * N, "coef must hold scale[N] and shift[N]");
-  c10::DeviceGuard dg(A.device());
-  int sk = split_k > 0 ? (int)split_k : dtg::gemm_pick_split(M, N, K, 0);
-  Tensor ws;
-  float* wsp = nullptr;
-  if (sk > 1) {
-    ws = at::empty({dtg::gemm_workspace_floats(M, N, K, sk)}, A.options().dtype(at::kFloat));
-    wsp = ws.data_ptr<float>();
-  }
-  dtg::gemm_bf16_xb(cbfp(A), A.stride(0), cbfp(B), B.stride(0), out.data_ptr(), out.stride(0),
-                    out.scalar_type() == at::kBFloat16, M, N, K, (float)beta, coef.data_ptr<float>(), sk, wsp,
-                    cur_stream());
 }
 
 std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64_t pad, bool pooled) {
@@ -691,10 +580,8 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
   auto part = bn_part(x, K, pooled);
-  // The direct halo-tile conv for 3x3 / s1 / p1, 64 -> 64 (ResNet-50 layer 1)
-  // (conv_halo.hip, bound as conv_halo_fwd_bn): 16 % faster alone (338 vs 400 us at batch 1024 with the
-  // statistics), but it holds all of every CU's LDS while it runs, and the whole training step measured no
-  // faster (profiles/r03_conv_l2), so the implicit GEMM is the path here
+  // (The direct halo-tile conv for 3x3 / s1 / p1, 64 -> 64, was 16 % faster alone but no faster in the training
+  // step, profiles/r03_conv_l2: it lives in the lab extension, csrc/lab/conv_halo.hip.)
   dtg::BnEpi bn;
   bn.part = part.data_ptr<float>();
   bn.mode = 1;
@@ -969,60 +856,6 @@ void conv_wgrad(Tensor dy, Tensor x, Tensor dw, double beta, int64_t stride, int
                   ws.data_ptr<float>(), split, N, H, W, C, K, R, S, stride, pad, cur_stream(), sw, (int)sched);
 }
 
-// BN backward in two halves (the BN-folded 1x1 dgrads, models/resnet_fused.py): the finalize of the epilogue
-// partials -> coef [a, bx, c] (dx = a*dp + bx*x + c) and dgamma/dbeta accumulated ...
-Tensor bn_bwd_coef(Tensor part, Tensor gamma, Tensor smean, Tensor sinv, Tensor dgamma_acc, Tensor dbeta_acc, int64_t M) {
-  CHECK_IN(part);
-  CHECK_DT(part, at::kFloat);
-  const int C = (int)gamma.numel();
-  TORCH_CHECK(part.numel() == (long long)dtg::kBnStatSlots * 2 * C, "partials size mismatch");
-  for (const Tensor* t : {&gamma, &smean, &sinv, &dgamma_acc, &dbeta_acc}) {
-    CHECK_IN(*t);
-    CHECK_DT(*t, at::kFloat);
-    TORCH_CHECK(t->numel() == C, "per-channel tensor size mismatch");
-  }
-  c10::DeviceGuard dg(part.device());
-  auto coef = at::empty({3LL * C}, part.options());
-  dtg::bn_bwd_coef_from_part(part.data_ptr<float>(), gamma.data_ptr<float>(), smean.data_ptr<float>(),
-                             sinv.data_ptr<float>(), coef.data_ptr<float>(), dgamma_acc.data_ptr<float>(),
-                             dbeta_acc.data_ptr<float>(), M, C, 1, cur_stream());
-  return coef;
-}
-
-// ... and the dx pass from those coefficients
-Tensor bn_dx_coef(Tensor dp, Tensor x, Tensor coef) {
-  CHECK_IN(dp);
-  CHECK_IN(x);
-  CHECK_DT(dp, at::kBFloat16);
-  CHECK_DT(x, at::kBFloat16);
-  TORCH_CHECK(x.dim() == 2 && dp.sizes() == x.sizes() && x.size(1) % 8 == 0, "dp/x must be [M, C]");
-  CHECK_IN(coef);
-  CHECK_DT(coef, at::kFloat);
-  TORCH_CHECK(coef.numel() == 3 * x.size(1), "coef must be [3C]");
-  c10::DeviceGuard dg(x.device());
-  auto dx = at::empty_like(x);
-  dtg::bn_dx_from_coef(cbfp(dp), cbfp(x), coef.data_ptr<float>(), bfp(dx), nullptr, x.size(0), (int)x.size(1),
-                       cur_stream());
-  return dx;
-}
-
-// W [K, N] (a 1x1 conv weight [Cout, Cin] read as the dgrad's B operand) -> (Wab [2K, N] bf16, cw [N] fp32)
-std::tuple<Tensor, Tensor> bn_fold_weights(Tensor W, Tensor coef) {
-  CHECK_CUDA(W);
-  CHECK_DT(W, at::kBFloat16);
-  TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1, "W must be [K, N] with contiguous rows");
-  const int K = (int)W.size(0), N = (int)W.size(1);
-  CHECK_IN(coef);
-  CHECK_DT(coef, at::kFloat);
-  TORCH_CHECK(coef.numel() == 3LL * K, "coef must be [3K]");
-  c10::DeviceGuard dg(W.device());
-  auto Wab = at::empty({2LL * K, N}, W.options());
-  auto cw = at::empty({N}, coef.options());
-  dtg::bn_fold_weights(cbfp(W), W.stride(0), coef.data_ptr<float>(), bfp(Wab), cw.data_ptr<float>(), K, N,
-                       cur_stream());
-  return {Wab, cw};
-}
-
 }  // namespace
 
 void register_transformer_ops(pybind11::module_& m);  // transformer_ops.cc
@@ -1044,14 +877,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("out") = pybind11::none(), pybind11::arg("pooled") = false,
         pybind11::arg("x2") = pybind11::none(), pybind11::arg("mean2") = pybind11::none(),
         pybind11::arg("invstd2") = pybind11::none(), pybind11::arg("part2") = pybind11::none(),
-        pybind11::arg("sub2_hw") = pybind11::none(), pybind11::arg("xcoef") = pybind11::none(),
-        pybind11::arg("a2") = pybind11::none(), pybind11::arg("colbias") = pybind11::none());
-  m.def("bn_finalize", &bn_finalize, pybind11::arg("part"), pybind11::arg("gamma"), pybind11::arg("beta"),
-        pybind11::arg("rmean"), pybind11::arg("rvar"), pybind11::arg("M"), pybind11::arg("momentum"),
-        pybind11::arg("eps"));
-  m.def("conv_halo_fwd", &conv_halo_fwd, pybind11::arg("x"), pybind11::arg("w"));
-  m.def("gemm_xb", &gemm_xb, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("out"), pybind11::arg("coef"),
-        pybind11::arg("beta") = 0.0, pybind11::arg("split_k") = 0);
+        pybind11::arg("sub2_hw") = pybind11::none());
   m.def("bn_part_alloc", [](Tensor like, int64_t C, bool pooled) { return bn_part(like, C, pooled); },
         pybind11::arg("like"), pybind11::arg("C"), pybind11::arg("pooled") = false);
   m.def("bn_bwd2_part", &bn_bwd2_part, pybind11::arg("dp"), pybind11::arg("x"), pybind11::arg("part"),
@@ -1061,7 +887,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none(),
         pybind11::arg("wact2") = pybind11::none(), pybind11::arg("wgrad2") = pybind11::none());
   m.def("bn_dx_wgrad_ok", [](int64_t M, int64_t C, int64_t CI) { return dtg::bn_dx_wgrad_ok(M, (int)C, (int)CI); });
-  m.def("conv_halo_fwd_bn", &conv_halo_fwd_bn, pybind11::arg("x"), pybind11::arg("w"));
   m.def("conv_fwd_bn", &conv_fwd_bn, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"),
         pybind11::arg("pad"), pybind11::arg("pooled") = false);
   m.def("conv_dgrad_bn", &conv_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("H"),
@@ -1082,9 +907,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("gamma"), pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("want_dres"),
         pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none(),
         pybind11::arg("wact") = pybind11::none(), pybind11::arg("wgrad") = pybind11::none());
-  m.def("bn_bwd_coef", &bn_bwd_coef);
-  m.def("bn_dx_coef", &bn_dx_coef);
-  m.def("bn_fold_weights", &bn_fold_weights);
   m.doc() = "dtg gfx950 HIP kernels";
   m.def("sgd_apply", &sgd_apply);
   m.def("momentum_apply", &momentum_apply);
@@ -1094,6 +916,34 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("comm_spin", [](double seconds, int64_t wgs, int64_t lds_bytes) {
     dtg::comm_spin(seconds, (int)wgs, (int)lds_bytes, cur_stream());
   }, pybind11::arg("seconds"), pybind11::arg("wgs") = 32, pybind11::arg("lds_bytes") = 0);
+  m.def("comm_emu", [](double seconds, int64_t wgs, int64_t mode, c10::optional<Tensor> scratch, int64_t base,
+                       int64_t traffic_bytes, c10::optional<Tensor> bucket, double factor) {
+    // scratch: a contiguous byte buffer (traffic mode); bucket: the contiguous fp32 / bf16 gradient slice (data mode)
+    long long sbytes = 0, n = 0;
+    int bf = 0;
+    const Tensor* dev_t = nullptr;
+    if (scratch.has_value() && scratch->defined()) {
+      CHECK_IN(*scratch);
+      TORCH_CHECK(((uintptr_t)scratch->data_ptr() % 16) == 0, "scratch: 16-B aligned");
+      sbytes = scratch->numel() * scratch->element_size();
+      dev_t = &*scratch;
+    }
+    if (bucket.has_value() && bucket->defined()) {
+      CHECK_IN(*bucket);
+      TORCH_CHECK(bucket->scalar_type() == at::kFloat || bucket->scalar_type() == at::kBFloat16, "bucket fp32/bf16");
+      n = bucket->numel();
+      bf = bucket->scalar_type() == at::kBFloat16;
+      dev_t = &*bucket;
+    }
+    TORCH_CHECK(!(mode & 2) || sbytes > 0, "traffic mode needs scratch");
+    TORCH_CHECK(!(mode & 4) || n > 0 || !(bucket.has_value() && bucket->defined()), "data mode needs the bucket");
+    c10::optional<c10::DeviceGuard> dg;
+    if (dev_t) dg.emplace(dev_t->device());
+    return dtg::comm_emu(seconds, (int)wgs, (int)mode, sbytes ? scratch->data_ptr() : nullptr, sbytes, base,
+                         traffic_bytes, n ? bucket->data_ptr() : nullptr, n, bf, (float)factor, cur_stream());
+  }, pybind11::arg("seconds"), pybind11::arg("wgs") = 32, pybind11::arg("mode") = 0,
+        pybind11::arg("scratch") = pybind11::none(), pybind11::arg("base") = 0, pybind11::arg("traffic_bytes") = 0,
+        pybind11::arg("bucket") = pybind11::none(), pybind11::arg("factor") = 1.0);
   m.def("hyper_tick", [](Tensor hyper) {
     check_hyper(hyper);
     c10::DeviceGuard dg(hyper.device());
@@ -1159,7 +1009,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("smean"), pybind11::arg("sinv"), pybind11::arg("relu"), pybind11::arg("want_dres"),
         pybind11::arg("dgamma_acc") = pybind11::none(), pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("softmax_xent", &softmax_xent);
-  m.def("gemm_force_cfg", [](int64_t c) { dtg::gemm_force_cfg((int)c); });
   m.def("gemm_bn_force_cfg", [](int64_t c) { dtg::gemm_bn_force_cfg((int)c); });
   m.def("conv_force_tile", [](int64_t which, int64_t c) { dtg::conv_force_tile((int)which, (int)c); });
   m.def("conv_set_stages", [](int64_t which, int64_t s) { dtg::conv_set_stages((int)which, (int)s); });

@@ -92,11 +92,6 @@ __device__ __forceinline__ void epilogue_bn_stream(lds_char* smem, f32x4 (&acc)[
       }
     }
   }
-  // modes 3/4 with a folded BN (BnEpi::colbias): the constant row added to every accumulator
-  float cb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if constexpr (MODE == 3 || MODE == 4) {
-    if (bn.colbias && n0 < N) load8_f32(bn.colbias + n0, cb);
-  }
   if constexpr (MODE == 1 || MODE == 5) {
     epilogue_staged<C>(smem, acc, bm0, bn0, M, N, [&](int m, int n, float (&v)[8]) {
       const int row = rowmap(m);
@@ -140,7 +135,7 @@ __device__ __forceinline__ void epilogue_bn_stream(lds_char* smem, f32x4 (&acc)[
         if (e.beta != 0.f && bn_row_has_old(bn, row)) load8_bf16((const bf16_t*)e.C + off, old);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float d = mk[k] > 0.f ? fmaf(v[k] + cb[k], e.alpha, e.beta * old[k]) : 0.f;
+          const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
           v[k] = d;
           s[k] += d;
           q[k] += d * xv[k];
@@ -200,7 +195,7 @@ __device__ __forceinline__ void epilogue_bn_stream(lds_char* smem, f32x4 (&acc)[
         if (ho[j]) unpack8_bf16(po[j], old);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float d = mk[k] > 0.f ? fmaf(v[k] + cb[k], e.alpha, e.beta * old[k]) : 0.f;
+          const float d = mk[k] > 0.f ? fmaf(v[k], e.alpha, e.beta * old[k]) : 0.f;
           v[k] = d;
           s[k] += d;
           q[k] += d * xv[k];

@@ -185,16 +185,6 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
   store8_bf16(p, v);
 }
 
-// 256x256 8-wave 8-phase GEMM (gemm8.hip); same operand conventions as gemm_bf16, no batching
-void gemm8_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, const Epi& e,
-                int M, int N, int K, int split_k, int kps, float* ws, hipStream_t st);
-
-// persistent 256x256 8-phase GEMM (gemm8.hip gemm8p_kernel): bf16 out, K-contiguous A, epilogues plain /
-// bias / bias+GELU with GELU' saved / x aux; false (nothing launched) when the problem or epilogue does not fit
-// (abl: timing ablations for the A/B tool, forced configs 97 / 96)
-bool gemm8p_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, const Epi& e,
-                 int M, int N, int K, hipStream_t st, int abl = 0);
-
 // split-K reduction of fp32 slabs [split][M][N] + the epilogue (gemm.hip)
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st);
 

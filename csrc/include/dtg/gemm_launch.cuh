@@ -11,10 +11,7 @@
 namespace dtg {
 using namespace gemm;
 
-// XF: operand prologue (mfma_gemm.cuh XfA / XfB) with its coefficients in bn.xcoef / bn.xc_n: 0 none,
-// 1 the A operand (BN mode 1 forward GEMMs), 2 the B operand (weight gradients, gemm_bf16_xb)
-template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false, bool BNPF = false,
-          int XF = 0>
+template <class CF, bool AKC, bool BKC, class SA, class SB, int BNMODE = 0, bool FAST = false, bool BNPF = false>
 __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA sa, SB sb, int M, int N, int K, int tiles_n, int split_k,
                                                      int k_per_split, Epi e, float* __restrict__ ws, GemmBatch bt,
                                                      BnEpi bn) {
@@ -51,15 +48,7 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (XF == 1) {
-    mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc, XfA{bn.xcoef, bn.xc_n});
-  } else if constexpr (XF == 2) {
-    XfB<CF::BN, CF::NW> xf;
-    xf.init(bn.xcoef, bn.xc_n, bn0, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63);
-    mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc, xf);
-  } else {
-    mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
-  }
+  mainloop<CF, AKC, BKC>(sa, sb, smem, bm0, bn0, kbeg, kend, acc);
   if constexpr (BNMODE != 0) {  // (no split-K, no batching: gemm_bf16_bn)
     // one tile per workgroup, the column statistics live only in the epilogue.  (Several M tiles per
     // workgroup, statistics carried across their main loops, ran ResNet-50 3-4 % slower: the gemm bn3

@@ -31,6 +31,10 @@ void fill_zero(void* p, long long bytes, hipStream_t st);
 
 // ---- emulated blocking collective (comm_emu.hip; parallel/ddp.py DTG_COMM_EMULATE) ------------------
 void comm_spin(double seconds, int wgs, int lds_bytes, hipStream_t st);
+// round-5 form: mode bits 1 busy-poll, 2 HBM traffic through scratch (base: window offset, advanced by the returned
+// count), 4 data (bucket *= factor after the wait)
+long long comm_emu(double seconds, int wgs, int mode, void* scratch, long long scratch_bytes, long long base,
+                   long long traffic_bytes, void* buf, long long n, int buf_bf16, float factor, hipStream_t st);
 void launch_probe(int grid, int lds_bytes, hipStream_t st);
 // HBM streaming probe (stream_probe.hip): kind 0 read, 1 write, 2 copy, 3 read2/write1 over n16 16-B vectors
 void stream_probe(int kind, const void* a, const void* b, void* o, long long n16, unsigned* sink, int wgs, int unroll,
@@ -69,18 +73,6 @@ struct BnEpi {
   // (magic m, shift l of H*W and of W, host-computed: bn_sub2_rows).
   int old_sub2 = 0;
   uint32_t old_hw = 1, old_w = 1, hw_m = 0, hw_l = 0, w_m = 0, w_l = 0;
-  // optional operand prologue: a BatchNorm apply + ReLU, relu(v * xcoef[c] + xcoef[xc_n + c]), applied to the
-  // fragments of the operand that holds the previous BN's raw input (channel c), so the BN output is never
-  // written to memory (gemm_bf16_bn mode 1: the A operand, c = k; gemm_bf16_xb: the B operand, c = column)
-  const float* xcoef = nullptr;
-  int xc_n = 0;
-  // mode 3/4, optional (BN-folded dgrad): the A operand is the K-concatenation [A | a2] -- columns k < ka1 from
-  // A, k >= ka1 from a2 (same rows, row stride lda2; ka1 % 64 == 0) -- and colbias[n] is added to every
-  // accumulator before the relu mask / residual add (batchnorm.hip bn_fold_weights)
-  const bf16_t* a2 = nullptr;
-  long long lda2 = 0;
-  int ka1 = 0;
-  const float* colbias = nullptr;
 };
 
 // host: fill the old_sub2 fields of a BnEpi for an H x W image
@@ -104,11 +96,6 @@ long long bn_workspace_floats(long long M, int C);
 void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* gamma, const float* beta,
                       float* rmean, float* rvar, float* smean, float* sinv, const float* part, float* ws, long long M,
                       int C, float momentum, float eps, int relu, hipStream_t st, uint8_t* bits = nullptr);
-// statistics from epilogue partials -> smean / sinv, running stats, coef = (scale[C], shift[C]); no apply pass
-// (the consumer GEMM applies relu(x * scale + shift) to its operand fragments: BnEpi::xcoef)
-void bn_finalize_part(const float* part, const float* gamma, const float* beta, float* rmean, float* rvar,
-                      float* smean, float* sinv, float* coef, long long M, int C, float momentum, float eps,
-                      hipStream_t st);
 // y = relu(bn(x) + bn2(r)) with both BNs' statistics from epilogue partials (ws: 4C floats)
 void bn_fwd2_from_part(const bf16_t* x, const bf16_t* r, bf16_t* y, const float* part, const float* part2,
                        const float* gamma, const float* beta, float* rmean, float* rvar, float* smean, float* sinv,
@@ -125,9 +112,6 @@ void bn_bwd2_from_part(const bf16_t* dp, const bf16_t* x, const bf16_t* x2, cons
 void bn_bwd_coef_from_part(const float* part, const float* gamma, const float* smean, const float* sinv, float* coef,
                            float* dgamma, float* dbeta, long long M, int C, int accum, hipStream_t st);
 void bn_dx_from_coef(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_t* dx, bf16_t* dres, long long M, int C,
-                     hipStream_t st);
-// Wab = [diag(a) W ; diag(bx) W] ([2K][N] bf16), cw = c^T W ([N] fp32) for coef = [a, bx, c] (batchnorm.hip)
-void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
                      hipStream_t st);
 // bn_dx_wgrad.hip: the dx pass (from bn_bwd_coef_from_part coefficients, optionally the projection shortcut's dx2
 // from the same dp) fused with the weight gradient dW += dx^T act of the conv that produced x (C x CI = 256 x 64 or
@@ -165,8 +149,8 @@ struct GemmBatch {
   int count = 1, nh = 1;
   long long sa_b = 0, sa_h = 0, sb_b = 0, sb_h = 0, sc_b = 0, sc_h = 0;
 };
-// force one GEMM tile configuration (sweeps; 0 = heuristic, 99 = 8-phase 256x256)
-void gemm_force_cfg(int cfg);
+// force the BN-epilogue GEMM tile (tools/bn_gemm_ab.py; 0 = heuristic).  (Forced tiles of the plain GEMM and the
+// 256x256 8-phase kernels live in the lab extension, csrc/lab.)
 void gemm_bn_force_cfg(int cfg);
 void conv_force_tile(int which, int code);  // conv.hip: 0 fwd, 1 stride-1 dgrad
 long long gemm_workspace_floats(int M, int N, int K, int split_k);
@@ -179,17 +163,6 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 // (bn.mode 1: B is [N,K] (forward); bn.mode 2/3: B is [K,N] (dgrad)).  A is [M,K] K-contiguous.
 void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st);
-// C (+)= A^T op(B) for MN-contiguous A [K,M] and B [K,N] (a weight gradient, split-K over K) where B is the
-// raw input of a BatchNorm + ReLU: the GEMM reads relu(B * coef[n] + coef[N + n]) (coef from
-// bn_finalize_part) instead of the materialised BN output
-void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, void* C, long long ldc, int c_bf16,
-                  int M, int N, int K, float beta, const float* coef, int split_k, float* ws, hipStream_t st);
-// Direct 3x3 / stride 1 / pad 1 conv for C = K = 64 from an LDS halo tile (conv_halo.hip); with part, also the
-// BatchNorm forward statistics of the output (BnEpi mode 1 partials, kBnStatSlots x 2 x 64)
-int conv3x3_halo_supported(int C, int K, int H, int W, int stats = 0);
-void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st,
-                      float* part = nullptr);
-
 // C = act(A * B + bias) (B [K,N], the dgrad layout; aux as in gemm_bf16) and colsum[n] += sum_m C[m, n]
 // in the same epilogue (fp32 atomics; the bias gradient of the layer C is the output gradient of)
 void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,

@@ -97,27 +97,6 @@ struct DenseKC {
     return sel(k < K, p + (long long)r * ld + k);
   }
 };
-// KC operand concatenated along K from two matrices with the same rows: k < K1 from p, k >= K1 from p2 (K1 a
-// multiple of the 64-deep K-step, so a step never straddles the two and the pick is wave-uniform)
-template <bool GUARD>
-struct DenseKC2 {
-  static constexpr bool kGuard = GUARD;
-  const bf16_t* p;
-  long long ld;
-  int rows, K;
-  const bf16_t* p2;
-  long long ld2;
-  int K1;
-  __device__ __forceinline__ const void* chunk(int row, int k) const {
-    const bool second = k >= K1;
-    const bf16_t* base = second ? p2 : p;
-    const long long l = second ? ld2 : ld;
-    const int kk = second ? k - K1 : k;
-    if constexpr (!GUARD) return base + (long long)row * l + kk;
-    const int r = row < rows ? row : rows - 1;
-    return sel(k < K, base + (long long)r * l + kk);
-  }
-};
 // MC: matrix stored [K][ld] with the row/col (M or N) index contiguous
 template <bool GUARD>
 struct DenseMC {
@@ -246,118 +225,13 @@ __device__ __forceinline__ void compute_tile(const lds_char* At, const lds_char*
   }
 }
 
-// ---- operand prologue: BatchNorm apply + ReLU on a staged operand tile (BnEpi::xcoef) ---------------
-// The GEMM reads the BN's raw input x and uses relu(x * scale[c] + shift[c]) (fp32, rounded to bf16: the
-// value the standalone apply pass would have written), so that BN output never goes through HBM.  Each lane
-// transforms, in LDS, exactly the 16-byte chunks its own LDS-DMA wrote: after its own vmcnt wait those bytes
-// are visible to it (MI355X_MICROARCH.md item 7), and the barrier that follows publishes the transformed
-// tile to the other waves -- so every element is transformed once per workgroup, with no extra barrier.
-//   XfNone: plain operands
-//   XfA:    the K-contiguous A operand, channel c = k (1x1 conv forward: A = the previous BN's input).  A
-//           lane's chunk is always the same logical 8-channel group of the K-step (stage_kc's swizzle makes
-//           it (lane & 7) ^ (lane >> 3)): its 16 coefficients are loaded with the step's DMA.
-//   XfB:    the MN-contiguous B operand, channel c = column n (weight gradient: B = that same input).  The
-//           columns a lane stages never change along K: their coefficients are loaded once.
-struct XfNone {
-  static constexpr int kind = 0;
-};
-struct XfA {
-  static constexpr int kind = 1;
-  const float* coef;  // [scale[n], shift[n]]
-  int n;
-};
-template <int ROWS, int NW>
-struct XfB {
-  static constexpr int kind = 2;
-  static constexpr int CH = ROWS / 8, KPI = 64 / CH, PER_WAVE = 64 / KPI / NW;
-  float sc[PER_WAVE][8], sh[PER_WAVE][8];
-  // col0: the tile's first column; channel = column (ncols = number of columns / coefficient stride)
-  __device__ __forceinline__ void init(const float* coef, int ncols, int col0, int wave, int lane) {
-#pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i) {
-      const int kr = (wave * PER_WAVE + i) * KPI + lane / CH;
-      const int col = col0 + ((lane % CH) ^ mc_swz<CH>(kr)) * 8;
-      if (col < ncols) {
-        load8_f32(coef + col, sc[i]);
-        load8_f32(coef + ncols + col, sh[i]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sc[i][k] = sh[i][k] = 0.f;
-      }
-    }
-  }
-};
-
-__device__ __forceinline__ v8bf affine_relu8(v8bf f, const float (&sc)[8], const float (&sh)[8]) {
-  const u32x4 u = __builtin_bit_cast(u32x4, f);
-  float x[8];
-  x[0] = __uint_as_float(u.x << 16); x[1] = __uint_as_float(u.x & 0xffff0000u);
-  x[2] = __uint_as_float(u.y << 16); x[3] = __uint_as_float(u.y & 0xffff0000u);
-  x[4] = __uint_as_float(u.z << 16); x[5] = __uint_as_float(u.z & 0xffff0000u);
-  x[6] = __uint_as_float(u.w << 16); x[7] = __uint_as_float(u.w & 0xffff0000u);
-  u32x4 o;
-  o.x = pack_bf2(fmaxf(fmaf(x[0], sc[0], sh[0]), 0.f), fmaxf(fmaf(x[1], sc[1], sh[1]), 0.f));
-  o.y = pack_bf2(fmaxf(fmaf(x[2], sc[2], sh[2]), 0.f), fmaxf(fmaf(x[3], sc[3], sh[3]), 0.f));
-  o.z = pack_bf2(fmaxf(fmaf(x[4], sc[4], sh[4]), 0.f), fmaxf(fmaf(x[5], sc[5], sh[5]), 0.f));
-  o.w = pack_bf2(fmaxf(fmaf(x[6], sc[6], sh[6]), 0.f), fmaxf(fmaf(x[7], sc[7], sh[7]), 0.f));
-  return __builtin_bit_cast(v8bf, o);
-}
-
-// the XfA coefficients of this lane's chunk for the K-step at k0 (issued together with the step's DMA)
-__device__ __forceinline__ void xfa_load(const XfA& xf, int k0, int lane, float (&sc)[8], float (&sh)[8]) {
-  const int c = k0 + 8 * ((lane & 7) ^ (lane >> 3));
-  if (c < xf.n) {
-    load8_f32(xf.coef + c, sc);
-    load8_f32(xf.coef + xf.n + c, sh);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sc[k] = sh[k] = 0.f;
-  }
-}
-
-// transform the chunks stage_kc<ROWS, ., NW, 64> made this lane write (after its vmcnt wait)
-template <int ROWS, int NW>
-__device__ __forceinline__ void xfa_fix(lds_char* tile, const float (&sc)[8], const float (&sh)[8], int wave, int lane) {
-  constexpr int PER_WAVE = ROWS / (8 * NW);
-#pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    lds_v8bf* p = reinterpret_cast<lds_v8bf*>(tile + (wave * PER_WAVE + i) * 8 * 128 + lane * 16);
-    *p = affine_relu8(*p, sc, sh);
-  }
-}
-
-// transform the chunks stage_mc<ROWS, ., NW, 64> made this lane write
-template <int ROWS, int NW>
-__device__ __forceinline__ void xfb_fix(lds_char* tile, const XfB<ROWS, NW>& xf, int wave, int lane) {
-  using X = XfB<ROWS, NW>;
-#pragma unroll
-  for (int i = 0; i < X::PER_WAVE; ++i) {
-    lds_v8bf* p = reinterpret_cast<lds_v8bf*>(tile + (wave * X::PER_WAVE + i) * X::KPI * ROWS * 2 + lane * 16);
-    *p = affine_relu8(*p, xf.sc[i], xf.sh[i]);
-  }
-}
-
 // ---- main loop -------------------------------------------------------------------------------
 // Accumulates the K range [kbeg, kend) into acc[4][4].  STA(tile, k0) / STB(tile, k0) issue the
 // LDS-DMA of one 64-deep K-step of the A / B operand into an LDS tile (generic stagers below,
 // or implicit-GEMM gathers in conv.hip).
-// XF: operand prologue (XfA / XfB above; the single-stage schedules only: there every wave waits for its
-// own DMA before the barrier that publishes the tile, which is where the transform goes)
-template <class C, bool AKC, bool BKC, class STA, class STB, class XF = XfNone>
+template <class C, bool AKC, bool BKC, class STA, class STB>
 __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_char* smem, int kbeg, int kend,
-                                            f32x4 (&acc)[4][4], const XF& xf = XF()) {
-  static_assert(XF::kind == 0 || C::STAGES == 1, "operand prologue: single-stage schedules only");
-  static_assert(XF::kind != 1 || (AKC && C::BK == 64), "A prologue: K-contiguous A, 64-deep steps");
-  static_assert(XF::kind != 2 || (!BKC && C::BK == 64), "B prologue: MN-contiguous B, 64-deep steps");
-  float xsc[8], xsh[8];  // XfA: this lane's coefficients for the K-step in flight
-  auto xf_pre = [&](int k0) {
-    if constexpr (XF::kind == 1) xfa_load(xf, k0, threadIdx.x & 63, xsc, xsh);
-  };
-  auto xf_fix = [&]() {  // after this wave's vmcnt wait, before the barrier
-    const int ln = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if constexpr (XF::kind == 1) xfa_fix<C::BM, C::NW>(smem, xsc, xsh, wv, ln);
-    if constexpr (XF::kind == 2) xfb_fix<C::BN, C::NW>(smem + C::A_BYTES, xf, wv, ln);
-  };
+                                            f32x4 (&acc)[4][4]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
@@ -378,9 +252,7 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
     };
     sta(smem, kbeg);
     stb(smem + C::A_BYTES, kbeg);
-    xf_pre(kbeg);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    xf_fix();
     __syncthreads();
     read_frags();
     __syncthreads();  // every wave holds its fragments: the LDS buffer is free for the next DMA
@@ -389,7 +261,6 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
       if (more) {
         sta(smem, kbeg + (kt + 1) * BK);
         stb(smem + C::A_BYTES, kbeg + (kt + 1) * BK);
-        xf_pre(kbeg + (kt + 1) * BK);
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -400,7 +271,6 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][i], b[ks][j], acc[i][j], 0, 0, 0);
       if (more) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        xf_fix();
         __syncthreads();
         read_frags();
         __syncthreads();
@@ -410,9 +280,7 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
     for (int kt = 0; kt < nk; ++kt) {
       sta(smem, kbeg + kt * BK);
       stb(smem + C::A_BYTES, kbeg + kt * BK);
-      xf_pre(kbeg + kt * BK);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      xf_fix();
       __syncthreads();
       compute_tile<C, AKC, BKC>(smem, smem + C::A_BYTES, wm, wn, lane, acc);
       __syncthreads();
@@ -471,15 +339,15 @@ __device__ __forceinline__ void mainloop_st(const STA& sta, const STB& stb, lds_
   }
 }
 
-template <class C, bool AKC, bool BKC, class SA, class SB, class XF = XfNone>
+template <class C, bool AKC, bool BKC, class SA, class SB>
 __device__ __forceinline__ void mainloop(const SA& sa, const SB& sb, lds_char* smem, int bm0, int bn0, int kbeg,
-                                         int kend, f32x4 (&acc)[4][4], const XF& xf = XF()) {
+                                         int kend, f32x4 (&acc)[4][4]) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   mainloop_st<C, AKC, BKC>(
       [&](lds_char* t, int k0) { stage<AKC, C::BM, SA, C::NW, C::BK>(sa, t, bm0, k0, wave, lane); },
       [&](lds_char* t, int k0) { stage<BKC, C::BN, SB, C::NW, C::BK>(sb, t, bn0, k0, wave, lane); },
-                           smem, kbeg, kend, acc, xf);
+                           smem, kbeg, kend, acc);
 }
 
 // ---- fast integer division by a runtime constant (Granlund-Montgomery), n < 2^31 --------------

@@ -346,14 +346,6 @@ void bn_fwd_from_part(const bf16_t* x, const bf16_t* res, bf16_t* y, const float
   bn_apply_launch(g, x, res, y, ws, M, C, relu, st, bits);
 }
 
-// Finalize only: the BN output is produced by its consumer GEMM's operand prologue (BnEpi::xcoef)
-void bn_finalize_part(const float* part, const float* gamma, const float* beta, float* rmean, float* rvar,
-                      float* smean, float* sinv, float* coef, long long M, int C, float momentum, float eps,
-                      hipStream_t st) {
-  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, 0, gamma, beta, rmean, rvar, smean,
-                                                    sinv, momentum, eps, coef, nullptr, nullptr, 1); DTG_LAUNCH_CHECK();
-}
-
 // Inference: coefficients from running statistics (tiny launch) then the same apply pass.
 __global__ void bn_infer_coef_kernel(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                                      float eps, int C, float* coef) {
@@ -529,51 +521,6 @@ void bn_bwd_from_part(const bf16_t* dp, const bf16_t* x, const float* gamma, con
                       int C, int accum, hipStream_t st) {
   bn_bwd_coef_from_part(part, gamma, smean, sinv, ws, dgamma, dbeta, M, C, accum, st);
   bn_dx_from_coef(dp, x, ws, dx, dres, M, C, st);
-}
-
-// BN backward folded into the following 1x1 data gradient.  With dy = a*dp + bx*x + c per channel k (coef),
-//   dx[p, n] = sum_k dy[p, k] W[k, n] = sum_k dp[p, k] (a_k W[k, n]) + sum_k x[p, k] (bx_k W[k, n]) + sum_k c_k W[k, n]
-// so the dgrad is ONE GEMM over the K-concatenation [dp | x] with the weights [diag(a) W ; diag(bx) W] (rounded to
-// bf16 once here) plus the constant row cw = c^T W (fp32, added in the epilogue) -- no dx pass over HBM.
-// W [K][N] (row stride ldw); Wab [2K][N] contiguous.  Block = 64 columns x 4 row slices (one wave each): lanes
-// take consecutive columns (coalesced rows), each wave a quarter of the rows, 8 rows of loads in flight; the
-// four slices' partial cw meet in LDS in slice order (deterministic).
-__global__ void __launch_bounds__(256) bn_fold_weights_kernel(const bf16_t* __restrict__ W, long long ldw,
-                                                              const float* __restrict__ coef, bf16_t* __restrict__ Wab,
-                                                              float* __restrict__ cw, int K, int N) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + lane;
-  const int k0 = (int)((long long)K * sl / 4), k1 = (int)((long long)K * (sl + 1) / 4);
-  float s = 0.f;
-  if (n < N) {
-    int k = k0;
-    for (; k + 8 <= k1; k += 8) {
-      float w[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) w[u] = bf2f(W[(long long)(k + u) * ldw + n]);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        Wab[(long long)(k + u) * N + n] = f2bf(coef[k + u] * w[u]);
-        Wab[(long long)(K + k + u) * N + n] = f2bf(coef[K + k + u] * w[u]);
-        s = fmaf(coef[2 * K + k + u], w[u], s);
-      }
-    }
-    for (; k < k1; ++k) {
-      const float w = bf2f(W[(long long)k * ldw + n]);
-      Wab[(long long)k * N + n] = f2bf(coef[k] * w);
-      Wab[(long long)(K + k) * N + n] = f2bf(coef[K + k] * w);
-      s = fmaf(coef[2 * K + k], w, s);
-    }
-  }
-  part[sl][lane] = s;
-  __syncthreads();
-  if (sl == 0 && n < N) cw[n] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-}
-
-void bn_fold_weights(const bf16_t* W, long long ldw, const float* coef, bf16_t* Wab, float* cw, int K, int N,
-                     hipStream_t st) {
-  bn_fold_weights_kernel<<<(N + 63) / 64, 256, 0, st>>>(W, ldw, coef, Wab, cw, K, N); DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -133,15 +133,10 @@ static void launch_cfg(int a_kc, int b_kc, const bf16_t* A, long long lda, const
   }
 }
 
-// (The 256x256 8-wave 8-phase kernel, gemm8.hip, lost to the 128x128 single-stage kernels on every flagship
-// shape -- BERT's MLM decoder 30528x768x5120 wgrad 419 vs 289 us, 5120x768x30528 dgrad 834 vs 286 us split 2,
-// profiles/r02_gemm -- and the 256x128 8-wave 3-slot ring on every shape of profiles/r01_gemm_ab: both are
-// reachable only through the forced-configuration table, gemm_force_cfg, for the A/B tools.)
+// (The 256x256 8-wave 8-phase kernel and the forced-configuration table that measured every tile against this
+// heuristic -- BERT's MLM decoder 30528x768x5120 wgrad 419 vs 289 us, 5120x768x30528 dgrad 834 vs 286 us split 2,
+// profiles/r02_gemm -- live in the tools-only lab extension, csrc/lab.)
 
-// forced tile configurations (tools/gemm_sweep.py): gemm_forced.hip
-bool gemm_launch_forced(int cfg, int a_kc, int b_kc, const bf16_t* A, long long lda, const bf16_t* B, long long ldb,
-                        int M, int N, int K, int split_k, int kps, const Epi& e, float* ws, hipStream_t st,
-                        const GemmBatch& bt);
 // Register pipelining pays when each workgroup has a long K loop and the problem is compute-heavy
 // enough that latency, not occupancy (3 instead of 4 workgroups per CU), limits it: long K (>= 2048),
 // or K >= 768 at >= 300 flop per operand byte (BERT's 8192-token GEMMs: 5-12 % faster; ResNet's
@@ -156,11 +151,6 @@ static bool use_rp(int M, int N, int kps) {
   const double flop = 2.0 * M * N * kps, bytes = 2.0 * ((double)M * kps + (double)N * kps + (double)M * N);
   return kps >= 768 && flop / bytes >= 300.0;
 }
-
-// forced tile configuration for the A/B tools (tools/gemm_ab.py, gemm_sweep.py): 0 = the heuristics below
-static int g_forced_cfg = 0;
-static int forced_cfg() { return g_forced_cfg; }
-void gemm_force_cfg(int cfg) { g_forced_cfg = cfg; }
 
 void gemm_splitk_reduce(const float* ws, int split_k, int M, int N, const Epi& e, hipStream_t st) {
   if (N % 8 == 0 && split_k > 16) {
@@ -184,16 +174,6 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
   split_k = (K + kps - 1) / kps;
   if (split_k < 1) split_k = 1;
   Epi e{C, ldc, c_bf16, alpha, beta, bias, act, aux, aux_mode};
-  if (const int fc = forced_cfg()) {
-    if (fc >= 96 && fc <= 98 && bt.count == 1 && split_k == 1 &&
-        gemm8p_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, st, 98 - fc))
-      return;
-    if (fc == 99 && bt.count == 1) {
-      gemm8_bf16(A, lda, a_kc, B, ldb, b_kc, e, M, N, K, split_k, kps, ws, st);
-      return;
-    }
-    if (gemm_launch_forced(fc, a_kc, b_kc, A, lda, B, ldb, M, N, K, split_k, kps, e, ws, st, bt)) return;
-  }
   if (split_k > 1 || !a_kc) {
     // weight gradients (MN-contiguous A, split-K over the token/pixel dimension): the single-stage
     // 128x128 ring beat every other tile and the 2-stage ring on all of them, BERT's 768x3072x8192
@@ -232,25 +212,15 @@ void gemm_bf16(const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long l
 }
 
 // ---- BN-statistics epilogue (gemm_bf16_bn) ---------------------------------------------------------
-template <class CF, int MODE, bool GUARD, bool PF, int XF = 0>
+template <class CF, int MODE, bool GUARD, bool PF>
 static void launch_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
                       const Epi& e, const BnEpi& bn, hipStream_t st) {
   using SB = std::conditional_t<MODE == 1, DenseKC<GUARD>, DenseMC<GUARD>>;
   SB sb{B, ldb, N, K};
   const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  if constexpr (MODE == 3 || MODE == 4) {
-    if (bn.a2) {  // BN-folded dgrad: A = [A | a2] along K
-      using SA2 = DenseKC2<GUARD>;
-      SA2 sa{A, lda, M, K, bn.a2, bn.lda2, bn.ka1};
-      hipLaunchKernelGGL((gemm_kernel<CF, true, false, SA2, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
-                         dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn);
-      DTG_LAUNCH_CHECK();
-      return;
-    }
-  }
   using SA = DenseKC<GUARD>;
   SA sa{A, lda, M, K};
-  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF, XF>), dim3(tiles_m * tiles_n, 1, 1),
+  hipLaunchKernelGGL((gemm_kernel<CF, true, MODE == 1, SA, SB, MODE, false, PF>), dim3(tiles_m * tiles_n, 1, 1),
                      dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, 1, K, e, (float*)nullptr, GemmBatch(), bn); DTG_LAUNCH_CHECK();
 }
 
@@ -311,23 +281,6 @@ static void gemm_bn_dispatch(const bf16_t* A, long long lda, const bf16_t* B, lo
   else launch_bn_cfg<Cfg<128, 128, 1>, MODE>(A, lda, B, ldb, M, N, K, e, bn, st);
 }
 
-// mode 1 with the previous BN applied to A in the operand prologue (BnEpi::xcoef, mfma_gemm.cuh XfA): the
-// single-stage tiles only (the prologue's coefficient loads must not wait behind an in-flight LDS-DMA), with
-// gemm_bn_dispatch's tile choice otherwise
-template <class CF>
-static void launch_bn_xa(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
-                         const Epi& e, const BnEpi& bn, hipStream_t st) {
-  if ((M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0)) launch_bn<CF, 1, false, false, 1>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else launch_bn<CF, 1, true, false, 1>(A, lda, B, ldb, M, N, K, e, bn, st);
-}
-
-static void gemm_bn_xa_dispatch(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
-                                const Epi& e, const BnEpi& bn, hipStream_t st) {
-  if (skinny(N)) launch_bn_xa<Cfg<256, 64, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else if (N >= 256 && K > 128 && K <= 256 && M >= 64) launch_bn_xa<Cfg<64, 256, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
-  else launch_bn_xa<Cfg<128, 128, 1>>(A, lda, B, ldb, M, N, K, e, bn, st);
-}
-
 // gemm_expand.hip: persistent streaming GEMM + statistics for short-K, wide-N forward 1x1 convs
 bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long ldw, bf16_t* C, long long ldc, int M,
                     int N, int K, float* part, hipStream_t st, int variant);
@@ -336,8 +289,7 @@ void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
                   int N, int K, float beta, const BnEpi& bn, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   Epi e{C, ldc, 1, 1.f, bn.mode == 3 ? beta : 0.f, nullptr, 0};
-  if (bn.mode == 1 && bn.xcoef) gemm_bn_xa_dispatch(A, lda, B, ldb, M, N, K, e, bn, st);
-  else if (bn.mode == 1) {
+  if (bn.mode == 1) {
     if ((g_bn_gemm_cfg == 0 || g_bn_gemm_cfg <= -2) &&
         gemm_expand_bn(A, lda, B, ldb, C, ldc, M, N, K, bn.part, st, g_bn_gemm_cfg == 0 ? 0 : -1 - g_bn_gemm_cfg))
       return;
@@ -346,42 +298,6 @@ void gemm_bf16_bn(const bf16_t* A, long long lda, const bf16_t* B, long long ldb
   else if (bn.mode == 2) gemm_bn_dispatch<2>(A, lda, B, ldb, M, N, K, e, bn, st);
   else if (bn.x2) gemm_bn_dispatch<4>(A, lda, B, ldb, M, N, K, e, bn, st);
   else gemm_bn_dispatch<3>(A, lda, B, ldb, M, N, K, e, bn, st);
-}
-
-// ---- weight gradient with the B operand's BN + ReLU in the prologue (gemm_bf16_xb) -------------------
-template <class CF, bool GUARD>
-static void launch_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K, int split_k,
-                      int kps, const Epi& e, const BnEpi& bn, float* ws, hipStream_t st) {
-  using S = DenseMC<GUARD>;
-  S sa{A, lda, M, K};
-  S sb{B, ldb, N, K};
-  const int tiles_m = (M + CF::BM - 1) / CF::BM, tiles_n = (N + CF::BN - 1) / CF::BN;
-  hipLaunchKernelGGL((gemm_kernel<CF, false, false, S, S, 0, false, false, 2>), dim3(tiles_m * tiles_n, split_k, 1),
-                     dim3(CF::NTH), 0, st, sa, sb, M, N, K, tiles_n, split_k, kps, e, ws, GemmBatch(), bn); DTG_LAUNCH_CHECK();
-  if (split_k > 1) gemm_splitk_reduce(ws, split_k, M, N, e, st);
-}
-
-template <class CF>
-static void launch_xb_cfg(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, int M, int N, int K,
-                          int split_k, int kps, const Epi& e, const BnEpi& bn, float* ws, hipStream_t st) {
-  if ((M % CF::BM == 0) && (N % CF::BN == 0) && (K % BK == 0)) launch_xb<CF, false>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
-  else launch_xb<CF, true>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
-}
-
-void gemm_bf16_xb(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, void* C, long long ldc, int c_bf16,
-                  int M, int N, int K, float beta, const float* coef, int split_k, float* ws, hipStream_t st) {
-  if (M <= 0 || N <= 0) return;
-  if (split_k < 1) split_k = 1;
-  int kps = (K + split_k - 1) / split_k;
-  kps = (kps + BK - 1) / BK * BK;
-  if (kps < BK) kps = BK;
-  split_k = (K + kps - 1) / kps;
-  Epi e{C, ldc, c_bf16, 1.f, beta, nullptr, 0};
-  BnEpi bn;
-  bn.xcoef = coef;
-  bn.xc_n = N;
-  // the weight-gradient tile of gemm_bf16 (single-stage 128x128, register-pipelined)
-  launch_xb_cfg<Cfg<128, 128, 1, 4, 64, true>>(A, lda, B, ldb, M, N, K, split_k, kps, e, bn, ws, st);
 }
 
 void gemm_bf16_colsum(const bf16_t* A, long long lda, const bf16_t* B, long long ldb, bf16_t* C, long long ldc, int M,

@@ -13,6 +13,7 @@
 
 #include "dtg/common.h"
 #include "dtg/kernels.h"
+#include "lab.h"
 #include "dtg/mfma_gemm.cuh"
 
 namespace dtg {

@@ -22,6 +22,7 @@
 // All LDS is one __shared__ array (a second LDS object can make hipcc drain vmcnt each step).
 #include "dtg/common.h"
 #include "dtg/kernels.h"
+#include "lab.h"
 #include "dtg/mfma_gemm.cuh"
 #include "dtg/gemm_epi.cuh"
 #include <type_traits>

@@ -2,6 +2,7 @@
 // tools/gemm_ab.py measure the heuristic in gemm.hip against.  Split over three translation units
 // (gemm_forced*.hip) so the instantiations compile in parallel.
 #include "dtg/gemm_launch.cuh"
+#include "lab.h"
 
 namespace dtg {
 

@@ -61,20 +61,10 @@ _LINK = True  # cross-block BN3 reduction (needs _FUSE)
 # linked stride-2 projection: its dgrad writes only the even (h, w) rows, which the next mode-3 GEMM alone
 # reads (no zero-fill of a [N, H, W, C] gradient per stage transition); 0 restores the zero-filled form
 _SUB2 = True
-# _BN2X = True: BN2 (+ relu) applied in conv3's operand prologues instead of a separate apply pass (needs
-# _FUSE): the forward GEMM reads y2 and the BN2 coefficients (gemm_bn xcoef), the weight gradient likewise
-# (gemm_xb); a2 and BN2's relu-mask bits are never written.  Off by default: measured slower, ResNet-50 b512
-# 14.46k vs 14.80k img/s -- the prologue costs the forward GEMMs +0.39 ms and the weight gradients +1.2 ms
-# per step against the 0.55 ms apply pass it removes (profiles/r03_bn2_prologue).
-_BN2X = False
-# _FOLD = True (round-4 experiment, off): BN3 (identity blocks) and BN1 backward folded into the following 1x1
-# dgrad -- the dgrad GEMM reads [dp | y] along K against [diag(a) W ; diag(bx) W] plus the constant row c^T W
-# (dy = a*dp + bx*y + c), so the main stream makes no dx pass for them; the weight gradient, which needs dy itself,
-# gets it from a dx pass on the side stream (batchnorm.hip bn_fold_weights, gemm_bn(a2=..., colbias=...)).
-# Measured 14.2k vs 15.2k img/s at b1024 (profiles/r04_bn_fold): the main stream shortened by 2.3 ms, but the
-# doubled-K dgrads took +3.4 ms and the side stream's dx passes (16 ms there) made it the critical path.  What
-# would remove them is a weight gradient reading [dp | y] with two accumulators (a_k G1 + bx_k G2 + c_k colsum x).
-_FOLD = False
+# (Round-3/4 experiments, removed in round 5 with their kernels -- git history has them: BN2 + relu applied in
+# conv3's operand prologues instead of an apply pass, 14.46k vs 14.80k img/s at b512 (profiles/r03_bn2_prologue);
+# BN3 / BN1 backward folded into the following 1x1 dgrads over [dp | y] along K, 14.2k vs 15.2k at b1024
+# (profiles/r04_bn_fold).)
 # _DXW = True: where the shape allows (stage 1: 256 x 64, bn_dx_wgrad_ok), conv3's weight gradient is computed inside
 # BN3's dx pass on the main stream (csrc/kernels/bn_dx_wgrad.hip) instead of re-reading dx on the side stream:
 # the backward is HBM-bound across both streams, and that re-read cost 0.3 ms of step per block
@@ -122,18 +112,14 @@ _CWSPLIT_WGS = int(os.environ.get("DTG_RESNET_CWSPLIT_WGS", "256"))
 _wsplit_cache = {}
 
 
-def _wgrad(dy, x, out, xcoef=None):
-    """out (+)= dy^T x for [P, M] dy and [P, N] x (P pixels): a 1x1 conv weight gradient.  With xcoef the
-    conv's input is relu(x * scale + shift) (a BN apply the forward never materialised, bn_finalize)."""
+def _wgrad(dy, x, out):
+    """out (+)= dy^T x for [P, M] dy and [P, N] x (P pixels): a 1x1 conv weight gradient."""
     tgt = _WSPLIT_WGS if overlap.enabled() else 0
     key = (dy.shape[1], x.shape[1], dy.shape[0], tgt)
     sk = _wsplit_cache.get(key)
     if sk is None:
         sk = _wsplit_cache[key] = lib().gemm_pick_split(key[0], key[1], key[2], False, tgt) if tgt > 0 else 0
-    if xcoef is not None:
-        lib().gemm_xb(dy, x, out, xcoef, 1.0, sk)
-    else:
-        gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
+    gemm(dy, False, x, False, out=out, beta=1.0, split_k=sk)
 
 
 def _conv_wgrad(dy4, x4, dw, st, pad):
@@ -164,21 +150,11 @@ class _BottleneckFn(torch.autograd.Function):
                                        b1.momentum, b1.eps, True, bits=bits1)
             y2, p2 = L.conv_fwd_bn(a1.view(n, h, w, width), _krsc(w2), st, 1, pooled=True)
             y2 = y2.view(-1, width)
-            if _BN2X:
-                # BN2 + relu applied in conv3's operand prologue (forward GEMM and weight gradient): a2 is never
-                # written; the backward recomputes BN2's relu mask from y2 (mode 2)
-                m2, i2, coef2 = L.bn_finalize(p2, b2.weight, b2.bias, b2.running_mean, b2.running_var, y2.shape[0],
-                                              b2.momentum, b2.eps)
-                a2 = bits2 = None
-                y3, p3 = L.gemm_bn(y2, _mat(w3), 1, pooled=True, xcoef=coef2)
-            else:
-                bits2 = _relu_bits(y2)
-                a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
-                                           b2.momentum, b2.eps, True, bits=bits2)
-                coef2 = None
-                y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
+            bits2 = _relu_bits(y2)
+            a2, m2, i2 = L.bn_fwd_part(y2, p2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var,
+                                       b2.momentum, b2.eps, True, bits=bits2)
+            y3, p3 = L.gemm_bn(a2, _mat(w3), 1, pooled=True)
             ctx.bits12 = (bits1, bits2)
-            ctx.coef2 = coef2
         else:
             y1 = gemm(x2, True, _mat(w1), True)
             a1, m1, i1 = L.bn_fwd_train(y1, None, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.momentum,
@@ -187,7 +163,6 @@ class _BottleneckFn(torch.autograd.Function):
             a2, m2, i2 = L.bn_fwd_train(y2, None, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.momentum,
                                         b2.eps, True)
             y3 = gemm(a2, True, _mat(w3), True)
-            ctx.coef2 = None
         yd = md = idd = None
         if blk.down is not None:
             bd, wd = blk.down.bn, blk.down.conv.weight
@@ -248,7 +223,6 @@ class _BottleneckFn(torch.autograd.Function):
         # BN3 (+ residual, relu): dres is the gradient flowing into the identity branch
         lk = ctx.link_out
         dyd = None
-        coef3 = None  # set when BN3's backward is folded into the conv3 dgrad (_FOLD)
         # conv3's weight gradient inside BN3's dx pass (_DXW)
         w3_kw = (dict(wact=a2, wgrad=g[id(w3)].view(cout, width))
                  if _DXW and a2 is not None and L.bn_dx_wgrad_ok(y3.shape[0], cout, width) else None)
@@ -267,8 +241,6 @@ class _BottleneckFn(torch.autograd.Function):
                                           sv[13], lk.part2, bd.weight, sv[14], sv[15], g[id(bd.weight)],
                                           g[id(bd.bias)], **kw)
                 w3_done = w3_kw is not None
-            elif _FOLD and bits12_ok(ctx):
-                coef3 = L.bn_bwd_coef(lk.part, b3.weight, m3, i3, g[id(b3.weight)], g[id(b3.bias)], y3.shape[0])
             else:
                 dy3 = L.bn_bwd_part(do, y3, lk.part, b3.weight, m3, i3, False, g[id(b3.weight)], g[id(b3.bias)],
                                     **(w3_kw or {}))[0]
@@ -285,25 +257,13 @@ class _BottleneckFn(torch.autograd.Function):
         # conv3 (1x1); with BN fusion its dgrad epilogue applies BN2's relu mask and reduces BN2's statistics
         bits1, bits2 = ctx.bits12 if _FUSE else (None, None)
         ctx.bits12 = None
-        if coef3 is not None:  # BN3 folded: A = [dp3 | y3], B = [diag(a) W3 ; diag(bx) W3], + c^T W3
-            w3ab, cw3 = L.bn_fold_weights(_mat(w3), coef3)
-            dp2, q2 = L.gemm_bn(do, w3ab, 3, y2, m2, i2, b2.weight, b2.bias, mask=bits2, pooled=True, a2=y3,
-                                colbias=cw3)
-        elif _FUSE and bits2 is not None:  # relu mask from the forward's bits: mode 3 with nothing to accumulate
+        if _FUSE and bits2 is not None:  # relu mask from the forward's bits: mode 3 with nothing to accumulate
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 3, y2, m2, i2, b2.weight, b2.bias, mask=bits2, pooled=True)
         elif _FUSE:
             dp2, q2 = L.gemm_bn(dy3, _mat(w3), 2, y2, m2, i2, b2.weight, b2.bias, pooled=True)
         else:
             da2 = gemm(dy3, True, _mat(w3), False)
-        coef2 = ctx.coef2
-        ctx.coef2 = None
-        if coef2 is not None:  # conv3's input is relu(bn2(y2)), applied in the weight-gradient GEMM's prologue
-            with overlap.wgrad_scope(dy3, y2, coef2):
-                _wgrad(dy3, y2, g[id(w3)].view(cout, width), coef2)
-        elif coef3 is not None:
-            with overlap.wgrad_scope(do, y3, coef3, a2):  # dy3 for the weight gradient only, off the main stream
-                _wgrad(L.bn_dx_coef(do, y3, coef3), a2, g[id(w3)].view(cout, width))
-        elif w3_done:
+        if w3_done:
             pass  # accumulated by BN3's dx pass above
         else:
             with overlap.wgrad_scope(dy3, a2):
@@ -329,10 +289,7 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.link_in = None
         if lk_in is not None and lk_in.y3.shape != x2.shape:
             lk_in = None
-        coef1 = dy1 = None
-        if _FUSE and _FOLD and lk_in is not None and bits12_ok(ctx):  # folded into the mode-3 conv1 dgrad below
-            coef1 = L.bn_bwd_coef(q1, b1.weight, m1, i1, g[id(b1.weight)], g[id(b1.bias)], y1.shape[0])
-        elif _FUSE:
+        if _FUSE:
             dy1 = L.bn_bwd_part(dp1, y1, q1, b1.weight, m1, i1, False, g[id(b1.weight)], g[id(b1.bias)])[0]
         else:
             dy1 = L.bn_bwd(da1, a1, y1, b1.weight, m1, i1, True, False, g[id(b1.weight)], g[id(b1.bias)])[0]
@@ -371,24 +328,14 @@ class _BottleneckFn(torch.autograd.Function):
                 part2 = None
                 if lk_in.yd is not None:  # the previous block is a projection block: its shortcut BN too
                     part2 = L.bn_part_alloc(dp1, c, pooled=True)
-                if coef1 is not None:  # BN1 folded: A = [dp1 | y1] against [diag(a) W1 ; diag(bx) W1], + c^T W1
-                    w1ab, cw1 = L.bn_fold_weights(_mat(w1), coef1)
-                    _, part = L.gemm_bn(dp1, w1ab, 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                        mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
-                                        invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw, a2=y1, colbias=cw1)
-                else:
-                    _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
-                                        mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
-                                        invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw)
+                _, part = L.gemm_bn(dy1, _mat(w1), 3, lk_in.y3, lk_in.m3, lk_in.i3, lk_in.gamma, lk_in.beta,
+                                    mask=lk_in.bits, out=dx2, pooled=True, x2=lk_in.yd, mean2=lk_in.md,
+                                    invstd2=lk_in.idd, part2=part2, sub2_hw=sub2_hw)
                 lk_in.part, lk_in.part2, lk_in.dp = part, part2, dx2
             else:
                 gemm(dy1, True, _mat(w1), False, out=dx2, beta=1.0)
-        if coef1 is not None:
-            with overlap.wgrad_scope(dp1, y1, coef1, x2):  # dy1 for the weight gradient only, off the main stream
-                _wgrad(L.bn_dx_coef(dp1, y1, coef1), x2, g[id(w1)].view(width, c))
-        else:
-            with overlap.wgrad_scope(dy1, x2):
-                _wgrad(dy1, x2, g[id(w1)].view(width, c))
+        with overlap.wgrad_scope(dy1, x2):
+            _wgrad(dy1, x2, g[id(w1)].view(width, c))
         if not all(direct for _, direct in accs):
             overlap.sync_current(x2.device)  # side-stream wgrads land in these before autograd adds them
         grads = []
@@ -399,11 +346,6 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 grads.append(a.to(p.dtype))
         return (dx2.view(n, h, w, c).permute(0, 3, 1, 2), None, None, None, *grads)
-
-
-def bits12_ok(ctx):
-    """BN folding needs the fused forward with its relu bits and epilogue statistics (not the BN2 prologue)."""
-    return _FUSE and _LINK and _BITS and not _BN2X
 
 
 def fused_ok(blk, x):

@@ -30,3 +30,21 @@ def available():
         return True
     except RuntimeError:
         return False
+
+
+_LAB = None
+
+
+def lab():
+    """The A/B lab extension ``dtg._lab`` (csrc/lab: kernels that are NOT part of the production ``_C`` --
+    negative results and main-loop candidates; build with ``python tools/build_ext.py --only lab``).  Its
+    kernels reuse production symbols of ``_C`` (e.g. the split-K reduction), so ``_C`` is first made global
+    (``RTLD_NOLOAD | RTLD_GLOBAL`` on the already-loaded library) before ``_lab`` is imported."""
+    global _LAB
+    if _LAB is None:
+        import ctypes
+        import os
+        c = lib()
+        ctypes.CDLL(c.__file__, mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL | os.RTLD_NOW)
+        _LAB = importlib.import_module("dtg._lab")
+    return _LAB

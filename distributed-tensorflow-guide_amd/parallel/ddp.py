@@ -28,14 +28,27 @@ from ..utils.trace import trace_range
 
 
 
+_EMU_MODES = {"busy": 1, "traffic": 2, "data": 4}
+
+
 def _parse_emulate(spec):
-    """DTG_COMM_EMULATE="<busbw GB/s>[,<ranks>[,<workgroups>[,<latency us>]]]" (defaults 8 ranks, 32
-    workgroups, 10 us).  See :meth:`DataParallel._emulate`."""
+    """DTG_COMM_EMULATE="<busbw GB/s>[,<ranks>[,<workgroups>[,<latency us>[,<modes>]]]]" (defaults 8 ranks, 32
+    workgroups, 10 us, no modes); modes = "+"-joined subset of busy, traffic, data (csrc/kernels/comm_emu.hip):
+    busy-polling waves, the ring's HBM traffic, and the bucket multiplied by the rank count (N identical
+    replicas summed).  See :meth:`DataParallel._emulate`."""
     if not spec:
         return None
-    f = [float(v) for v in spec.split(",")]
+    parts = spec.split(",")
+    modes = 0
+    if len(parts) >= 5:
+        for m in filter(None, parts[4].split("+")):
+            if m not in _EMU_MODES:
+                raise ValueError("DTG_COMM_EMULATE: unknown mode %r (busy, traffic, data)" % m)
+            modes |= _EMU_MODES[m]
+        parts = parts[:4]
+    f = [float(v) for v in parts]
     f += [8, 32, 10][len(f) - 1:]
-    return {"busbw_GBps": f[0], "ranks": int(f[1]), "wgs": int(f[2]), "latency_us": f[3]}
+    return {"busbw_GBps": f[0], "ranks": int(f[1]), "wgs": int(f[2]), "latency_us": f[3], "modes": modes}
 
 
 EMULATE = _parse_emulate(os.environ.get("DTG_COMM_EMULATE", ""))
@@ -67,6 +80,8 @@ class DataParallel:
         self._force = forced
         self._comm = True  # set_comm(False): gradients stay rank-local (bench.py's compute-only timing)
         self._estreams = {}
+        self._escratch = {}  # device index -> [scratch buffer, window offset] (traffic mode)
+        self._qprobe = {}    # device index -> out-of-place all-gather target (DTG_COMM_QUEUE_PROBE)
         # the emulated collective stands in for peers a one-rank run does not have: with real peers it would
         # add spin kernels on top of the real collectives and skew the scaling numbers, so it is refused there
         if EMULATE is not None and self.world > 1:
@@ -126,6 +141,13 @@ class DataParallel:
                 ls.wait_stream(main)
                 with torch.cuda.stream(ls):
                     b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                    if os.environ.get("DTG_COMM_QUEUE_PROBE") == "1" and self.world == 1:
+                        # one-rank out-of-place all-gather: RCCL copies on the process group's own stream, so a
+                        # kernel trace shows that stream's hardware queue (the in-place all-reduce issues nothing)
+                        out = self._qprobe.get(v.device.index)
+                        if out is None or out.numel() < v.numel() or out.dtype != v.dtype:
+                            out = self._qprobe[v.device.index] = torch.empty_like(v)
+                        dist.all_gather_into_tensor(out[:v.numel()], v, group=self.pg, async_op=True).wait()
                 self._emulate(v, ls)
                 return
             if side is not None:
@@ -140,23 +162,47 @@ class DataParallel:
         chip.  A one-rank collective is a local copy that never waits on a peer, so it cannot show whether the
         real one -- RCCL channel workgroups resident on CUs for the whole bus time, blocked on peers -- delays
         the backward's remaining weight gradients (the overlap that decides 1->8 scaling).  After the real
-        collective is enqueued, a spin kernel (csrc/kernels/comm_emu.hip) holding ``wgs`` workgroups for
+        collective is enqueued, an emulation kernel (csrc/kernels/comm_emu.hip) holding ``wgs`` workgroups for
         ``bytes * 2(N-1)/N / busbw + latency`` runs on a high-priority pool stream -- drawn from the same
         torch stream pool, at the same priority, as the process group's collective stream -- after everything
         the launching stream has queued; :meth:`finish` makes the main stream wait for it, as for the real
-        work.  Successive buckets serialise on that stream like collectives on RCCL's."""
+        work.  Successive buckets serialise on that stream like collectives on RCCL's.
+
+        Modes (round 5, the pessimistic forms): ``busy`` -- every wave busy-polls, as RCCL's primitives do;
+        ``traffic`` -- the workgroups stream 2 x 2(N-1)/N x bucket bytes (read + written) through a 1 GiB scratch
+        buffer over the emulated time, the HBM traffic the ring adds next to the HBM-bound backward; ``data``
+        -- after the wait the bucket is read and written back times N (N identical replicas summed), so a test
+        sees every gradient of the bucket final when the collective read it (the optimizer then scales by
+        1/N, :attr:`grad_scale`)."""
         e = self.emulate
         if e is None or after is None:
             return
         from ..ops._native import lib
-        es = self._estreams.get(v.device.index)
+        idx = v.device.index
+        es = self._estreams.get(idx)
         if es is None:
-            es = self._estreams[v.device.index] = torch.cuda.Stream(device=v.device, priority=-1)
+            es = self._estreams[idx] = torch.cuda.Stream(device=v.device, priority=-1)
         n = e["ranks"]
-        secs = v.numel() * v.element_size() * 2.0 * (n - 1) / n / (e["busbw_GBps"] * 1e9) + e["latency_us"] * 1e-6
+        nbytes = v.numel() * v.element_size()
+        secs = nbytes * 2.0 * (n - 1) / n / (e["busbw_GBps"] * 1e9) + e["latency_us"] * 1e-6
         es.wait_stream(after)
+        modes = e.get("modes", 0)
         with torch.cuda.stream(es):
-            lib().comm_spin(secs, e["wgs"], 0)
+            if modes == 0:
+                lib().comm_spin(secs, e["wgs"], 0)
+                return
+            scratch = None
+            traffic = 0
+            if modes & 2:
+                sc = self._escratch.get(idx)
+                if sc is None:
+                    sc = self._escratch[idx] = [torch.empty(1 << 30, dtype=torch.uint8, device=v.device), 0]
+                scratch = sc[0]
+                traffic = int(2 * nbytes * 2.0 * (n - 1) / n)
+            used = lib().comm_emu(secs, e["wgs"], modes, scratch, sc[1] if scratch is not None else 0, traffic,
+                                  v if modes & 4 else None, float(n))
+            if scratch is not None:
+                sc[1] += used
 
     def _on_direct(self, p):
         if p in self._param_bucket:
@@ -177,7 +223,10 @@ class DataParallel:
     # -- step ------------------------------------------------------------------------------------
     @property
     def grad_scale(self):
-        """Factor the optimizer applies to the summed gradients (1/world: mean)."""
+        """Factor the optimizer applies to the summed gradients (1/world: mean; the emulated data mode sums
+        ``ranks`` identical replicas, so 1/ranks there)."""
+        if self.emulate is not None and self.emulate.get("modes", 0) & 4:
+            return 1.0 / self.emulate["ranks"]
         return 1.0 / self.world
 
     def finish(self):

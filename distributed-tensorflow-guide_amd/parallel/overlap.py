@@ -51,7 +51,9 @@ import torch
 
 _ON = os.environ.get("DTG_WGRAD_STREAM", "1") != "0"
 _MULTI = os.environ.get("DTG_WGRAD_STREAM") == "2"  # also with several ranks (rehearsals)
-_PRIO = -1  # torch stream priority of the side stream: high (its own hardware queue, see above)
+# torch stream priority of the side stream: high (its own hardware queue, see above); DTG_SIDE_PRIO overrides it
+# (A/B runs together with bench.py's DTG_MAIN_PRIO, which runs the step itself on a stream of that priority)
+_PRIO = int(os.environ.get("DTG_SIDE_PRIO", "-1"))
 _side = {}      # device index -> side stream
 _main = {}      # device index -> the main stream of the backward the side work belongs to
 _pending = set()

@@ -13,6 +13,7 @@ import dtg  # noqa: E402,F401  (registers the package)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running multi-process test")
+    config.addinivalue_line("markers", "lab: lab-extension kernels (dtg._lab, csrc/lab), GPU only, run with -m lab")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -21,5 +22,5 @@ def pytest_collection_modifyitems(config, items):
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")
     for it in items:
-        if "gpu" in it.keywords:
+        if "gpu" in it.keywords or "lab" in it.keywords:
             it.add_marker(skip)

@@ -245,122 +245,6 @@ def test_mode3_packed_mask_bits():
 
 
 # ---- BN apply + relu in the consumer GEMM's operand prologue (mfma_gemm.cuh XfA / XfB) ----------------
-def _coef(n, dev, g):
-    """scale/shift with both signs, so the relu clamps a real fraction of the elements"""
-    sc = (torch.randn(n, generator=g) * 0.8).to(dev)
-    sh = (torch.randn(n, generator=g) * 0.5).to(dev)
-    return sc, sh, torch.cat([sc, sh]).contiguous()
-
-
-@pytest.mark.parametrize("M,N,K", [(4096, 256, 64), (2048, 512, 128), (1024, 1024, 256), (512, 2048, 512),
-                                   (1000, 256, 64), (4096, 64, 256)])
-def test_gemm_bn_xcoef_prologue(M, N, K):
-    """mode 1 with xcoef == mode 1 on the materialised relu(y * scale + shift) (bf16-rounded, as the
-    standalone apply pass writes it): output and statistics"""
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(M + N + K)
-    y = (torch.randn(M, K, generator=g) * 2).to(dev, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) * 0.1).to(dev, torch.bfloat16)
-    sc, sh, coef = _coef(K, dev, g)
-    a = torch.relu(y.float() * sc + sh).to(torch.bfloat16)
-    ref, part_ref = lib().gemm_bn(a, w, 1)
-    out, part = lib().gemm_bn(y, w, 1, xcoef=coef)
-    assert _rel(out, ref) < 2e-3  # the same operand up to fma-vs-mul+add rounding of a few elements
-    s, q = _bn_stats(part, N)
-    sr, qr = _bn_stats(part_ref, N)
-    assert _rel(s, sr) < 2e-3 and _rel(q, qr) < 2e-3
-    full = (a.float() @ w.float().t())
-    assert _rel(out, full) < 1e-2
-
-
-@pytest.mark.parametrize("P,M,N,beta,split", [(8192, 256, 64, 1.0, 4), (4096, 1024, 256, 1.0, 0), (3000, 512, 128, 0.0, 1),
-                                            (16384, 128, 512, 1.0, 8)])
-def test_gemm_xb_weight_gradient(P, M, N, beta, split):
-    """out (+)= dy^T relu(x * scale + shift) against the fp32 reference on the materialised operand"""
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(P + M + N)
-    dy = (torch.randn(P, M, generator=g) * 0.1).to(dev, torch.bfloat16)
-    x = (torch.randn(P, N, generator=g) * 2).to(dev, torch.bfloat16)
-    sc, sh, coef = _coef(N, dev, g)
-    a = torch.relu(x.float() * sc + sh).to(torch.bfloat16)
-    out0 = torch.randn(M, N, generator=g).to(dev)
-    out = out0.clone()
-    lib().gemm_xb(dy, x, out, coef, beta, split)
-    ref = beta * out0 + dy.float().t() @ a.float()
-    assert _rel(out, ref) < 2e-3
-
-
-def test_bn_finalize_matches_fwd_part():
-    """bn_finalize (no apply) returns the statistics and coefficients bn_fwd_part uses, and updates the
-    running statistics the same way"""
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(7)
-    M, N, K = 4096, 128, 64
-    L = lib()
-    a = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) * 0.2).to(dev, torch.bfloat16)
-    gamma = (torch.rand(N, generator=g) + 0.5).to(dev)
-    beta = (torch.randn(N, generator=g) * 0.2).to(dev)
-    rm1, rv1 = torch.zeros(N, device=dev), torch.ones(N, device=dev)
-    rm2, rv2 = rm1.clone(), rv1.clone()
-    y, part = L.gemm_bn(a, w, 1)
-    part2 = part.clone()
-    out, m, i = L.bn_fwd_part(y, part, None, gamma, beta, rm1, rv1, 0.1, 1e-5, True)
-    m2, i2, coef = L.bn_finalize(part2, gamma, beta, rm2, rv2, M, 0.1, 1e-5)
-    assert torch.equal(m, m2) and torch.equal(i, i2)
-    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
-    sc, sh = coef[:N], coef[N:]
-    assert torch.allclose(sc, gamma * i2, rtol=1e-6) and torch.allclose(sh, beta - m2 * sc, rtol=1e-5, atol=1e-6)
-    assert float(part2.abs().sum()) == 0.0  # the pooled slots go back zeroed
-    assert _rel(out, torch.relu(y.float() * sc + sh).to(torch.bfloat16)) < 1e-3
-
-
-@pytest.mark.parametrize("M,Kc,N,accum", [(4096, 256, 64, False), (2048, 64, 256, True), (1024, 512, 128, True),
-                                          (1000, 128, 512, False)])
-def test_bn_folded_dgrad(M, Kc, N, accum):
-    """BN backward folded into the following 1x1 dgrad (batchnorm.hip bn_fold_weights, gemm_bn(a2=, colbias=)):
-    [dp | y] x [diag(a) W ; diag(bx) W] + c^T W, then the mode-3 mask / residual / statistics epilogue, against
-    fp32 torch: dy = a*dp + bx*y + c from bn_bwd_coef, dx = dy W, masked."""
-    L = lib()
-    dev = torch.device("cuda")
-    g = torch.Generator(device="cpu").manual_seed(4)
-    dp = torch.randn(M, Kc, generator=g).to(dev, torch.bfloat16)
-    y = (torch.randn(M, Kc, generator=g) * 2 + 0.5).to(dev, torch.bfloat16)
-    W = (torch.randn(Kc, N, generator=g) / Kc ** 0.5).to(dev, torch.bfloat16)
-    # BN statistics of y and the (sum dp, sum dp*xhat) partials in slot 0
-    mean_y = y.float().mean(0)
-    inv_y = torch.rsqrt(y.float().var(0, unbiased=False) + 1e-5)
-    gam = (torch.rand(Kc, generator=g) + 0.5).to(dev)
-    part = torch.zeros(SLOTS, 2, Kc, device=dev)
-    part[0, 0] = dp.float().sum(0)
-    part[0, 1] = (dp.float() * (y.float() - mean_y) * inv_y).sum(0)
-    dgam, dbet = torch.zeros(Kc, device=dev), torch.zeros(Kc, device=dev)
-    coef = L.bn_bwd_coef(part.view(-1), gam, mean_y, inv_y, dgam, dbet, M)
-    a, bx, c = coef.view(3, Kc)
-    dy_ref = a * dp.float() + bx * y.float() + c
-    # the BN the dgrad output feeds (mode 3: its relu mask as bits, its statistics)
-    x = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
-    mean, inv, gamma, beta = _chan(N, dev, g)
-    mask = (torch.rand(M, N, generator=g) > 0.4).to(dev)
-    bits = (mask.view(M, N // 8, 8).to(torch.uint8) << torch.arange(8, device=dev, dtype=torch.uint8)).sum(-1)
-    bits = bits.to(torch.uint8).contiguous()
-    res = torch.randn(M, N, generator=g).to(dev, torch.bfloat16) if accum else None
-    Wab, cw = L.bn_fold_weights(W, coef)
-    out = res.clone() if accum else None
-    o, part_o = L.gemm_bn(dp, Wab, 3, x, mean, inv, gamma, beta, mask=bits, out=out, a2=y, colbias=cw)
-    torch.cuda.synchronize()
-    ref = dy_ref @ W.float() + (res.float() if accum else 0)
-    ref = torch.where(mask, ref, torch.zeros_like(ref))
-    assert _rel(o, ref) < 1.5e-2, _rel(o, ref)
-    s_ref = ref.sum(0)
-    q_ref = (ref * (x.float() - mean) * inv).sum(0)
-    s, q = _bn_stats(part_o, N)
-    assert _rel(s, s_ref) < 2e-2 and _rel(q, q_ref) < 2e-2
-    # the side-stream half: dy from the same coefficients
-    dy = L.bn_dx_coef(dp, y, coef)
-    assert _rel(dy, dy_ref) < 1e-2
-
-
 @pytest.mark.parametrize("dual", [False, True])
 @pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,CI", [(256, 64), (512, 128)])

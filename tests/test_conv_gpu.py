@@ -124,24 +124,3 @@ def test_stem_pack_pairs_matches_pad(N, C, H, W, pad, S):
     assert torch.equal(wgot.cpu(), wref)
 
 
-def test_conv_halo_fwd_matches_fp32_reference():
-    """Direct 3x3 conv from an LDS halo tile (csrc/kernels/conv_halo.hip, conv_fwd_bn's opt-in path for
-    64 -> 64 3x3 s1 convs): equals the fp32 convolution, image edges in every band; N = 40 at 56 x 56 gives 560 bands,
-    so the persistent workgroups walk two or three bands each through the double-buffered halo."""
-    import torch.nn.functional as F
-    from dtg.ops._native import lib
-    g = torch.Generator().manual_seed(5)
-    dev = torch.device("cuda")
-    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(dev, torch.bfloat16)
-    for n in (3, 40):
-        x = torch.randn(n, 56, 56, 64, generator=g).to(dev, torch.bfloat16)
-        y = lib().conv_halo_fwd(x, w)
-        ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
-        assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
-        # BN statistics epilogue (conv_fwd_bn's contract)
-        y2, part = lib().conv_halo_fwd_bn(x, w)
-        assert torch.equal(y2, y)
-        p = part.view(-1, 2, 64).sum(0)
-        yf = y.float().reshape(-1, 64)
-        assert ((p[0] - yf.sum(0)).norm() / yf.sum(0).norm()).item() < 1e-3
-        assert ((p[1] - (yf * yf).sum(0)).norm() / (yf * yf).sum(0).norm()).item() < 1e-3

@@ -33,15 +33,13 @@ def test_resnet_tiny_loss_decreases():
 
 @pytest.mark.parametrize("cin,width,stride", [(64, 64, 1), (256, 64, 1), (256, 128, 2), (512, 128, 1)])
 @pytest.mark.parametrize("flat", [False, True])
-@pytest.mark.parametrize("bn_fuse,bn2x", [(True, True), (True, False), (False, False)])
-def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, bn2x, monkeypatch):
+@pytest.mark.parametrize("bn_fuse", [True, False])
+def test_fused_bottleneck_matches_layerwise(cin, width, stride, flat, bn_fuse, monkeypatch):
     """The hand-written bottleneck backward (with and without BN statistics fused into the conv
-    epilogues, with and without BN2 applied in conv3's operand prologues) equals the layer-by-layer
-    autograd path."""
+    epilogues) equals the layer-by-layer autograd path."""
     from dtg.models.resnet import Bottleneck
     from dtg.models import resnet_fused
     monkeypatch.setattr(resnet_fused, "_FUSE", bn_fuse)
-    monkeypatch.setattr(resnet_fused, "_BN2X", bn2x)
     dev = torch.device("cuda")
     torch.manual_seed(0)
     blocks = []
@@ -396,15 +394,11 @@ def test_resnet50_full_network_matches_fp32_reference():
     assert bad_blk > 5 * _med(e_blk.values())
 
 
-@pytest.mark.parametrize("fold", [False, True])
-def test_bottleneck_chain_matches_fp32_reference(fold, monkeypatch):
+def test_bottleneck_chain_matches_fp32_reference():
     """Three fused bottleneck nodes in a row -- a projection block (stride 1), an identity block and a strided
     projection block, linked through the cross-block BN3 reduction -- against F.conv2d / F.batch_norm in fp32
-    with dtg's bf16 storage points emulated: output, input gradient and every parameter gradient.  ``fold``:
-    BN1 / BN3 backward folded into the 1x1 dgrads (resnet_fused._FOLD)."""
+    with dtg's bf16 storage points emulated: output, input gradient and every parameter gradient."""
     from dtg.models.resnet import Bottleneck
-    from dtg.models import resnet_fused
-    monkeypatch.setattr(resnet_fused, "_FOLD", fold)
     torch.manual_seed(0)
     dev = torch.device("cuda")
     chain = torch.nn.Module()

@@ -18,8 +18,6 @@ from dtg.ops._native import lib  # noqa: E402
 
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
-if os.environ.get("DTG_AB_GEMM_CFG"):
-    lib().gemm_force_cfg(int(os.environ["DTG_AB_GEMM_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
     which, sched = item.split(":")
     lib().conv_set_stages(int(which), int(sched))

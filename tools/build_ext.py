@@ -109,7 +109,9 @@ def _link(objs, out, cmd):
     os.replace(tmp, out)
 
 
-def build_C(jobs=8, verbose=False):
+def build_C(jobs=8, verbose=False, name="_C", kdir="kernels", bdir="bindings"):
+    """A torch extension from csrc/<kdir>/*.hip (hipcc, gfx950) and csrc/<bdir>/*.cc: the production kernels
+    (_C), or the A/B lab kernels (_lab: csrc/lab, tools only -- never imported by the package)."""
     tinc, tapi, tlib, cxx11 = _torch_paths()
     pyinc = sysconfig.get_paths()["include"]
     common = ["-O3", "-fPIC", "-std=c++17", f"-I{os.path.join(CSRC, 'include')}",
@@ -117,10 +119,10 @@ def build_C(jobs=8, verbose=False):
     hip_flags = common + [f"--offload-arch={ARCH}", "-ffp-contract=fast", "-Wno-unused-result",
                           "-munsafe-fp-atomics"]
     bind_flags = common + [f"-I{os.path.join(ROCM, 'include')}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_API_INCLUDE_EXTENSION_H",
-                           "-DTORCH_EXTENSION_NAME=_C", f"-I{tinc}", f"-I{tapi}", f"-I{pyinc}",
+                           f"-DTORCH_EXTENSION_NAME={name}", f"-I{tinc}", f"-I{tapi}", f"-I{pyinc}",
                            "-Wno-unused-parameter", "-Wno-deprecated-declarations"]
-    kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    binds = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cc")))
+    kern = sorted(glob.glob(os.path.join(CSRC, kdir, "*.hip")))
+    binds = sorted(glob.glob(os.path.join(CSRC, bdir, "*.cc")))
     hd = _headers_digest()
     os.makedirs(OBJ, exist_ok=True)
     objs, built = [], 0
@@ -131,7 +133,7 @@ def build_C(jobs=8, verbose=False):
             o, b = f.result()
             objs.append(o)
             built += b
-    out = os.path.join(PKG, "_C" + EXT)
+    out = os.path.join(PKG, name + EXT)
     if built or not os.path.exists(out):
         _link(objs, out, [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", f"-L{tlib}",
                           "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
@@ -163,7 +165,7 @@ def build_runtime(jobs=8, verbose=False):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", choices=["C", "runtime"], default=None)
+    ap.add_argument("--only", choices=["C", "runtime", "lab"], default=None)
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--clean", action="store_true")
@@ -174,6 +176,8 @@ def main(argv=None):
         print("built", build_runtime(a.j, a.verbose))
     if a.only in (None, "C"):
         print("built", build_C(a.j, a.verbose))
+    if a.only == "lab":  # the A/B lab extension: only on request (tools), never part of the package build
+        print("built", build_C(a.j, a.verbose, name="_lab", kdir="lab", bdir="lab"))
 
 
 if __name__ == "__main__":

@@ -11,6 +11,10 @@ ranks of those; then the same step runs again with DataParallel (small buckets, 
 all-reduces are in flight while backward still runs) and the flat gradients must equal the
 oracle.  After one fused optimizer step the replicas must hold bit-identical parameters.
 Runs on RCCL with one GPU per rank as well (leave DTG_BACKEND unset).
+
+One rank with DTG_DDP_FORCE=1 and DTG_COMM_EMULATE=<...>,<modes with data>: the emulated collective multiplies
+each bucket by N after its wait, so the flat gradient must equal N x the local gradient (the ordering check of
+side-stream weight gradients, main-stream BN-parameter gradients and the collective; tests/test_ddp_gpu.py).
 """
 import argparse
 import os
@@ -70,6 +74,12 @@ def main():
     # 2) the same step through DataParallel (hooks + grad sinks + overlapped bucket all-reduces)
     flat.zero_grad()
     dp = DataParallel(flat, bucket_mb=a.bucket_mb)
+    emu_data = dp.emulate is not None and dp.emulate.get("modes", 0) & 4
+    if emu_data:
+        # one rank, DTG_COMM_EMULATE data mode: each bucket's emulated collective returns N x the bucket (N
+        # identical replicas summed), reading it only after every gradient in it is final -- so the DP gradient
+        # must be N x the local one everywhere; a bucket launched too early would leave some gradients at 1x
+        oracle = [t * dp.emulate["ranks"] for t in oracle]
     loss_fn().backward()
     dp.finish()
     worst = 0.0
@@ -87,8 +97,8 @@ def main():
         assert torch.equal(ref, g.master), f"rank {rank}: replicas diverged after the step"
     dp.remove_hooks()
     if rank == 0:
-        print(f"ddp rehearsal ok: model={a.model} world={world} buckets={len(dp.buckets)} worst_rel_err={worst:.3e}",
-              flush=True)
+        print(f"ddp rehearsal ok: model={a.model} world={world} buckets={len(dp.buckets)} worst_rel_err={worst:.3e}"
+              + (f" emulated_ranks={dp.emulate['ranks']} (data mode)" if emu_data else ""), flush=True)
     comm.shutdown()
 
 

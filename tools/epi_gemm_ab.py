@@ -21,6 +21,7 @@ import torch  # noqa: E402
 
 import dtg  # noqa: E402,F401
 from dtg.ops._native import lib  # noqa: E402
+from _forced_gemm import forced_gemm  # noqa: E402
 
 
 def timeit(fn, iters):
@@ -54,20 +55,19 @@ def main():
     pre = torch.empty(T, F, device=dev, dtype=bf)
     dpre = torch.empty(T, F, device=dev, dtype=bf)
     gb1 = torch.zeros(F, device=dev)
-    cases = {
-        "ffn1_fwd": lambda: L.gemm(x, True, w1, True, f1, 1.0, 0.0, b1, 2, 0, pre, 3),
-        "ffn2_dgrad": lambda: L.gemm(df2, True, w2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 4, colsum=gb1),
-        "plain": lambda: L.gemm(x, True, w1, True, f1, 1.0, 0.0, None, 0, 0),
+    cases = {  # (the colsum epilogue of ffn2_dgrad is production-only: cfg 0)
+        "ffn1_fwd": lambda c: forced_gemm(c, x, True, w1, True, f1, 1.0, 0.0, b1, 2, 0, pre, 3),
+        "ffn2_dgrad": lambda c: L.gemm(df2, True, w2, False, dpre, 1.0, 0.0, None, 2, 0, pre, 4, colsum=gb1),
+        "plain": lambda c: forced_gemm(c, x, True, w1, True, f1, 1.0, 0.0, None, 0, 0),
     }
     cfgs = [int(c) for c in a.cfgs.split(",")]
     res = {k: {c: [] for c in cfgs} for k in cases}
     for _ in range(a.rounds):
         for name, fn in cases.items():
             for c in cfgs:
-                L.gemm_force_cfg(c)
-                fn()
-                res[name][c].append(timeit(fn, a.iters))
-    L.gemm_force_cfg(0)
+                f = (lambda fn=fn, c=c: fn(c))
+                f()
+                res[name][c].append(timeit(f, a.iters))
     fl = 2.0 * T * F * H
     for name in cases:
         out = {str(c): {"us": round(sorted(v)[len(v) // 2], 1), "TF/s": round(fl / (sorted(v)[len(v) // 2] * 1e6), 1)}

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Tile-configuration sweep of the MFMA GEMM on the ResNet-50 / BERT shapes (gemm_force_cfg):
+"""Tile-configuration sweep of the MFMA GEMM on the ResNet-50 / BERT shapes (production heuristic = cfg 0, forced tiles through the lab extension, tools/_forced_gemm.py):
 one line per (shape, config) with time, TB/s and TFLOP/s; the fastest config per shape is marked.
 This is the data the heuristic in csrc/kernels/gemm.hip (gemm_bf16) is fitted to.
 
@@ -18,6 +18,7 @@ import torch  # noqa: E402
 
 import dtg  # noqa: E402,F401
 from dtg.ops._native import lib  # noqa: E402
+from _forced_gemm import forced_gemm  # noqa: E402
 
 NAMES = {0: "heur", 1: "128x128s1", 2: "128x128s2", 3: "128x128s3", 4: "128x128s4", 5: "256x64s2", 6: "256x64s3",
          7: "256x64s4", 8: "256x128s3w8", 9: "256x128s2w8", 10: "128x256s2w8", 11: "128x256s3w8", 12: "64x256s2",
@@ -85,15 +86,13 @@ def main():
             if c in (5, 6, 7, 14, 20, 22, 27) and N > 64 and N % 64:
                 continue
             for split in splits:
-                L.gemm_force_cfg(c)
                 out = torch.zeros_like(C)
-                L.gemm(A, akc, B, bkc, out, 1.0, 0.0, None, 0, split)
+                forced_gemm(c, A, akc, B, bkc, out, 1.0, 0.0, None, 0, split)
                 if ref is None:
                     ref = out.float()
                 err = ((out.float() - ref).norm() / (ref.norm() + 1e-9)).item()
-                us = timeit(lambda: L.gemm(A, akc, B, bkc, C, 1.0, beta, None, 0, split))
+                us = timeit(lambda: forced_gemm(c, A, akc, B, bkc, C, 1.0, beta, None, 0, split))
                 rows.append((c if len(splits) == 1 else (c, split), us, err))
-        L.gemm_force_cfg(0)
         best = min(r[1] for r in rows)
         for c, us, err in rows:
             mark = " *" if us == best else ""

@@ -115,7 +115,6 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--json", default="")
     ap.add_argument("--conv-stages", default="", help="LDS ring depth of conv fwd,dgrad,wgrad, e.g. 1,1,2")
-    ap.add_argument("--gemm-cfg", type=int, default=0, help="force one GEMM tile config (gemm_sweep numbering)")
     a = ap.parse_args()
     import torch
     import dtg  # noqa: F401
@@ -126,8 +125,6 @@ def main():
     if a.conv_stages:
         for i, v in enumerate(a.conv_stages.split(",")):
             L.conv_set_stages(i, int(v))
-    if a.gemm_cfg:
-        L.gemm_force_cfg(a.gemm_cfg)
     dev = torch.device("cuda")
     records = []
     active = [False]
@@ -207,7 +204,7 @@ def main():
                      "lost_us": us - bound})
     rows.sort(key=lambda r: -r["lost_us"])
     covered = sum(r["us"] for r in rows)
-    print(f"uninstrumented step {clean_ms:.2f} ms (conv stages {a.conv_stages or 'default'}, gemm cfg {a.gemm_cfg})")
+    print(f"uninstrumented step {clean_ms:.2f} ms (conv stages {a.conv_stages or 'default'})")
     print(f"step {total:.0f} us; instrumented ops {covered:.0f} us; roofline bound of those "
           f"{sum(r['bound_us'] for r in rows):.0f} us")
     print(f"{'op':52s} {'calls':>5s} {'us':>8s} {'TF/s':>7s} {'TB/s':>6s} {'eff':>5s} {'lost us':>8s}")

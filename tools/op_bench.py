@@ -23,8 +23,6 @@ def main():
     a = [int(v) for v in sys.argv[2:]]
     iters = int(os.environ.get("ITERS", "20"))
     L = lib()
-    if os.environ.get("GEMM_CFG"):  # forced GEMM tile configuration (gemm_force_cfg), e.g. 98 = persistent 256x256
-        L.gemm_force_cfg(int(os.environ["GEMM_CFG"]))
     dev = torch.device("cuda")
     bf = torch.bfloat16
     if op in ("gemm", "gemm_bn1"):
