@@ -41,8 +41,8 @@ def test_bench_async_ps_mode_one_card():
 @pytest.mark.gpu
 def test_async_ps_token_waits_for_device_gradient():
     """The worker's request token leaves only when its gradient exists on the device: an event recorded behind
-    a 0.2 s device spin (comm_spin stands in for a slow backward) holds the token back 0.2 s, while the host
-    that submitted it returned at once (parallel/async_ps.py::_Announcer, _ready_event)."""
+    an 80 ms device spin (comm_spin stands in for a slow backward; it caps a spin at 100 ms) holds the token back
+    80 ms, while the host that submitted it returned at once (parallel/async_ps.py::_Announcer, _ready_event)."""
     import time
 
     import torch
@@ -60,14 +60,14 @@ def test_async_ps_token_waits_for_device_gradient():
     torch.cuda.synchronize()
     a = _Announcer(Ctl())
     t0 = time.perf_counter()
-    lib().comm_spin(0.2, 1, 0)  # the "backward" producing g is still running ...
+    lib().comm_spin(0.08, 1, 0)  # the "backward" producing g is still running ...
     g.add_(1.0)
     a.submit(3, 1, _ready_event([g]))
     t_submit = time.perf_counter() - t0
     a.close()
-    assert t_submit < 0.1, t_submit
+    assert t_submit < 0.05, t_submit
     assert sent and sent[0][:2] == (3, 1)
-    assert sent[0][2] - t0 >= 0.19, sent[0][2] - t0
+    assert sent[0][2] - t0 >= 0.075, sent[0][2] - t0
     assert g.float().mean().item() == 1.0
 
 
@@ -76,7 +76,7 @@ def test_async_ps_slow_worker_one_card():
     """1 PS + 3 workers on one card (gloo, device tensors staged through the host), worker 3's gradients
     delayed by a device spin before each push: the fast workers take proportionally more updates."""
     import json
-    env = dict(os.environ, DTG_BACKEND="gloo", DTG_GLOO_DEVICE="cuda", DTG_APS_TEST_SLOW="3:0.2")
+    env = dict(os.environ, DTG_BACKEND="gloo", DTG_GLOO_DEVICE="cuda", DTG_APS_TEST_SLOW="3:0.1")
     r = subprocess.run(["python", os.path.join(ROOT, "tools", "async_ps_slow_worker.py"), "--workers", "3",
                         "--seconds", "6"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]

@@ -25,7 +25,11 @@ from prof_summary import short  # noqa: E402
 
 
 def is_comm(name):
-    return "comm_spin" in name or "nccl" in name.lower() or "rccl" in name.lower()
+    """Collective-side dispatches: RCCL kernels, dtg's emulated collective (comm_spin / comm_emu), and -- under
+    DTG_COMM_QUEUE_PROBE=1 -- the one-rank all-gather's copy on the process group's stream (a ROCclr blit)."""
+    n = name.lower()
+    return ("comm_spin" in n or "comm_emu" in n or "nccl" in n or "rccl" in n or "copybuffer" in n
+            or "rocclr" in n)
 
 
 def union(iv):
