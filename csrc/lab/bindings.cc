@@ -12,7 +12,7 @@ namespace dtg {
 namespace lab {
 int gemm5_bf16(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int sched, hipStream_t st);
 int gemm5p_bf16(const bf16_t* A, const bf16_t* B, void* C, int c_bf16, int M, int N, int K, const float* bias, int act,
-                void* aux, int aux_mode, hipStream_t st);
+                void* aux, int aux_mode, hipStream_t st, int grid);
 }  // namespace lab
 }  // namespace dtg
 
@@ -40,7 +40,7 @@ bool gemm5(Tensor A, Tensor B, Tensor out, int64_t sched) {
 // persistent v5 (C = A B^T, A [M,K], B [N,K]) with the production epilogue arguments; false if the shape is not
 // served (M % 256, N % 192, K % 64)
 bool gemm5p(Tensor A, Tensor B, Tensor out, c10::optional<Tensor> bias, int64_t act, c10::optional<Tensor> aux,
-            int64_t aux_mode) {
+            int64_t aux_mode, int64_t grid) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && out.is_cuda(), "GPU tensors");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "bf16 operands");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out bf16 / fp32");
@@ -61,7 +61,8 @@ bool gemm5p(Tensor A, Tensor B, Tensor out, c10::optional<Tensor> bias, int64_t 
   }
   c10::DeviceGuard dg(A.device());
   return dtg::lab::gemm5p_bf16(cbfp(A), cbfp(B), out.data_ptr(), out.scalar_type() == at::kBFloat16, A.size(0),
-                               B.size(0), A.size(1), bptr, (int)act, auxp, (int)aux_mode, cur_stream()) != 0;
+                               B.size(0), A.size(1), bptr, (int)act, auxp, (int)aux_mode, cur_stream(),
+                               (int)grid) != 0;
 }
 
 // gemm (the production binding's operand conventions) through forced configuration `cfg`; false if the
@@ -134,7 +135,7 @@ PYBIND11_MODULE(_lab, m) {
   m.def("gemm5", &gemm5, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("out"), pybind11::arg("sched") = 1);
   m.def("gemm5p", &gemm5p, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("out"),
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("aux") = pybind11::none(),
-        pybind11::arg("aux_mode") = 0);
+        pybind11::arg("aux_mode") = 0, pybind11::arg("grid") = 0);
   m.def("gemm_cfg", &gemm_cfg, pybind11::arg("cfg"), pybind11::arg("A"), pybind11::arg("a_kc"), pybind11::arg("B"),
         pybind11::arg("b_kc"), pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 1,

@@ -383,13 +383,14 @@ namespace dtg {
 namespace lab {
 // persistent v5 with dtg's generic epilogue (bias, activation, aux, alpha / beta, bf16 or fp32 out)
 int gemm5p_bf16(const bf16_t* A, const bf16_t* B, void* C, int c_bf16, int M, int N, int K, const float* bias, int act,
-                void* aux, int aux_mode, hipStream_t st) {
+                void* aux, int aux_mode, hipStream_t st, int grid) {
   if (M % BM || N % BN || K % 64 || K < 64) return 0;
   int dev = 0, cus = 0;
   DTG_HIP_CHECK(hipGetDevice(&dev));
   DTG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int tiles_n = N / BN, tiles = (M / BM) * tiles_n;
-  const int G = tiles < cus ? tiles : cus;
+  int G = tiles < cus ? tiles : cus;
+  if (grid > 0 && grid < G) G = grid;  // (debug / A/B: fewer workgroups, more tiles each)
   Epi e{C, N, c_bf16, 1.f, 0.f, bias, act, aux, aux_mode};
   int epi = 3;
   if (c_bf16 && act == 0 && aux_mode == 0) epi = bias ? 1 : 0;

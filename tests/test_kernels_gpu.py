@@ -280,34 +280,3 @@ def test_gemm_short_m_tiles(M, N, K, a_kc, b_kc):
         assert ((out - ref).norm() / ref.norm()).item() < 1e-2, sk
 
 
-@pytest.mark.parametrize("b_kc", [True, False])
-def test_gemm_8phase_persistent(M, N, K, b_kc, forced_cfg):
-    """Persistent 256x256 8-phase kernel (forced configuration 98, gemm8.hip gemm8p_kernel) vs fp32 torch: one
-    and many K-tiles per tile (every iteration a tile seam at K = 64), a partial last round of tiles, both B
-    layouts, and its four register epilogues (plain, bias, bias + GELU with GELU' saved, x saved GELU')."""
-    from dtg.ops._native import lib
-    forced_cfg(98)
-    torch.manual_seed(0)
-    A = torch.randn(M, K, device="cuda").bfloat16()
-    B = torch.randn((N, K) if b_kc else (K, N), device="cuda").bfloat16()
-    bias = torch.randn(N, device="cuda")
-    ref = A.float() @ (B.float().t() if b_kc else B.float())
-
-    def rel(x, r):
-        return ((x.float() - r).norm() / r.norm()).item()
-
-    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    lib().gemm(A, True, B, b_kc, out, 1.0, 0.0, None, 0, 1)
-    assert rel(out, ref) < 1e-2
-    lib().gemm(A, True, B, b_kc, out, 1.0, 0.0, bias, 0, 1)
-    assert rel(out, ref + bias) < 1e-2
-    aux = torch.empty_like(out)
-    pre = ref + bias
-    lib().gemm(A, True, B, b_kc, out, 1.0, 0.0, bias, 2, 1, aux, 3)
-    assert rel(out, F.gelu(pre, approximate="tanh")) < 2e-2
-    p = pre.clone().requires_grad_()
-    F.gelu(p, approximate="tanh").backward(torch.ones_like(p))
-    assert rel(aux, p.grad) < 2e-2
-    sav = (torch.rand(M, N, device="cuda") + 0.5).bfloat16()
-    lib().gemm(A, True, B, b_kc, out, 1.0, 0.0, None, 0, 1, sav, 4)
-    assert rel(out, ref * sav.float()) < 1e-2
