@@ -111,7 +111,7 @@ def main(argv=None):
     from dtg.utils import StepTimer, trace_range
 
     def train_step(forward_loss, dp, opt):
-        """forward -> backward (bucketed all-reduce fired from inside) -> join -> fused apply, with roctx
+        """forward -> backward (bucketed all-reduce fired from inside) -> join + fused apply per bucket, with roctx
         ranges around each phase when DTG_TRACE=1 (dtg.utils.trace).  The backward is seeded with a cached
         1.0 (``loss.backward()`` would launch a framework fill kernel for it every step)."""
         seed = []
@@ -124,8 +124,9 @@ def main(argv=None):
             with trace_range("dtg.backward"):
                 loss.backward(seed[0])
             with trace_range("dtg.allreduce.join"):
-                dp.finish()
-            opt.step(grad_scale=dp.grad_scale)
+                # finish + apply, each bucket's slice applied as soon as its all-reduce has landed (parallel/ddp.py
+                # DataParallel.step): the applies overlap the collective tail
+                dp.step(opt)
             return loss
         return step
 

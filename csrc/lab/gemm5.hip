@@ -304,10 +304,14 @@ __global__ void __launch_bounds__(256, 1) g5p_kernel(const bf16_t* __restrict__ 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before the next m-tile's writes
     }
+    // (the compiler materialises fzero with VALU moves right before this asm, and it does not know the asm is an
+    // MFMA: without these wait states the first MFMA read the register's previous contents -- a fragment -- and
+    // left acc[0][0] of every later tile with garbage, tools/gemm5p_debug.py)
+    asm volatile("s_nop 4" ::"v"(fzero));
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(fzero));
+      for (int j = 0; j < TJ; ++j) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "+a"(acc[i][j]) : "v"(fzero));
     __builtin_amdgcn_s_barrier();  // every wave's slot reads are done before the next K-tile is written over them
     __builtin_amdgcn_sched_barrier(0);
   };

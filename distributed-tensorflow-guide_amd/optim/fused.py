@@ -27,7 +27,11 @@ class _FlatOptimizer:
     def _wd(self, g):
         return self.weight_decay if g.name in self.wd_groups else 0.0
 
-    def step(self, grad_scale=1.0, zero_grad=True):
+    def step(self, grad_scale=1.0, zero_grad=True, ranges=None):
+        """One optimizer step over every flat group.  ``ranges`` (DataParallel.step): a list of
+        (group, lo, hi, ready) covering the groups, applied in that order, each after ``ready()`` has made the
+        current stream wait for that slice's gradient (its bucket's collective) -- so the apply of the buckets
+        reduced early runs while the last bucket's collective is still on the wire."""
         from ..parallel import overlap
         overlap.join()  # side-stream weight gradients done before the apply reads them
         self.step_count += 1
@@ -36,8 +40,13 @@ class _FlatOptimizer:
                 K.hyper_tick(self.hyper)  # dtg kernel (no framework elementwise launch on the step)
             else:
                 self.hyper[1].add_(1.0)
-            for g in self.flat:
-                self._apply(g, grad_scale, zero_grad)
+            if ranges is None:
+                for g in self.flat:
+                    self._apply(g, grad_scale, zero_grad)
+            else:
+                for g, lo, hi, ready in ranges:
+                    ready()
+                    self._apply(_Slice(g, lo, hi), grad_scale, zero_grad)
 
     def state_dict(self):
         return {"step": self.step_count, "lr": self.lr,
@@ -50,6 +59,22 @@ class _FlatOptimizer:
         for g in self.flat:
             for k, v in sd.get("state", {}).get(g.name, {}).items():
                 g.state_buffer(k).copy_(v)
+
+
+class _Slice:
+    """A contiguous element range [lo, hi) of a flat group, with the group's name / buffers sliced alike (the
+    fused applies are elementwise, so applying a group slice by slice is bit-identical to applying it whole)."""
+
+    def __init__(self, g, lo, hi):
+        self._g, self.lo, self.hi = g, lo, hi
+        self.name = g.name
+        self.master = g.master[lo:hi]
+        self.grad = g.grad[lo:hi]
+        self.mirror = g.mirror[lo:hi] if g.mirror is not None else None
+        self.state = g.state
+
+    def state_buffer(self, key):
+        return self._g.state_buffer(key)[self.lo:self.hi]
 
 
 class FusedSGD(_FlatOptimizer):

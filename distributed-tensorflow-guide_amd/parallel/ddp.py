@@ -55,7 +55,7 @@ EMULATE = _parse_emulate(os.environ.get("DTG_COMM_EMULATE", ""))
 
 
 class _Bucket:
-    __slots__ = ("group", "start", "end", "params", "pending", "work", "index")
+    __slots__ = ("group", "start", "end", "params", "pending", "work", "index", "seq", "emu_event")
 
     def __init__(self, group, start, index):
         self.group = group
@@ -65,6 +65,8 @@ class _Bucket:
         self.pending = 0
         self.work = None
         self.index = index
+        self.seq = 0            # launch order within the step (DataParallel.step applies in that order)
+        self.emu_event = None   # DTG_COMM_EMULATE: the emulated collective of this bucket done
 
     def view(self):
         return self.group.grad[self.start:self.end]
@@ -121,9 +123,13 @@ class DataParallel:
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
+            b.emu_event = None
         self._done = set()
+        self._nlaunched = 0
 
     def _launch(self, b):
+        b.seq = self._nlaunched
+        self._nlaunched += 1
         v = b.view()
         side = overlap.pending_stream(v)
         with trace_range("dtg.allreduce.bucket%d" % b.index):  # roctx range (DTG_TRACE=1)
@@ -148,14 +154,14 @@ class DataParallel:
                         if out is None or out.numel() < v.numel() or out.dtype != v.dtype:
                             out = self._qprobe[v.device.index] = torch.empty_like(v)
                         dist.all_gather_into_tensor(out[:v.numel()], v, group=self.pg, async_op=True).wait()
-                self._emulate(v, ls)
+                b.emu_event = self._emulate(v, ls)
                 return
             if side is not None:
                 # host-staged backends (gloo): the main stream waits for the side stream (an event, no host
                 # sync) and the collective is enqueued from the main stream exactly as without it
                 torch.cuda.current_stream(v.device).wait_stream(side)
             b.work = dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-            self._emulate(v, torch.cuda.current_stream(v.device) if v.is_cuda else None)
+            b.emu_event = self._emulate(v, torch.cuda.current_stream(v.device) if v.is_cuda else None)
 
     def _emulate(self, v, after):
         """DTG_COMM_EMULATE: make a one-card run pay what an N-rank RCCL all-reduce of this bucket costs the
@@ -187,10 +193,12 @@ class DataParallel:
         secs = nbytes * 2.0 * (n - 1) / n / (e["busbw_GBps"] * 1e9) + e["latency_us"] * 1e-6
         es.wait_stream(after)
         modes = e.get("modes", 0)
+        ev = torch.cuda.Event()
         with torch.cuda.stream(es):
             if modes == 0:
                 lib().comm_spin(secs, e["wgs"], 0)
-                return
+                ev.record(es)
+                return ev
             scratch = None
             traffic = 0
             if modes & 2:
@@ -203,6 +211,8 @@ class DataParallel:
                                   v if modes & 4 else None, float(n))
             if scratch is not None:
                 sc[1] += used
+            ev.record(es)
+        return ev
 
     def _on_direct(self, p):
         if p in self._param_bucket:
@@ -245,6 +255,40 @@ class DataParallel:
         for es in self._estreams.values():
             torch.cuda.current_stream(es.device).wait_stream(es)
         self._reset()
+
+    def step(self, opt, zero_grad=True):
+        """finish() + opt.step(), with the apply overlapped with the collective tail: every bucket's slice of the
+        flat buffers is applied as soon as ITS all-reduce has landed (the main stream waits per bucket, in
+        launch order), so the applies of the buckets reduced during backward run while the last buckets -- the
+        layers backward reaches last, e.g. BERT's word embeddings -- are still on the wire.  Bit-identical to
+        finish() + opt.step(grad_scale=self.grad_scale) (the fused applies are elementwise)."""
+        if not (self.overlap and self._comm) or (self.world == 1 and not self._force):
+            self.finish()
+            return opt.step(grad_scale=self.grad_scale, zero_grad=zero_grad)
+        overlap.join()
+        for b in self.buckets:
+            if b.work is None:
+                self._launch(b)
+        order = sorted(self.buckets, key=lambda b: b.seq)
+        estreams = list(self._estreams.values())
+
+        def ready_fn(b):
+            def ready():
+                b.work.wait()
+                if b.emu_event is not None:
+                    torch.cuda.current_stream().wait_event(b.emu_event)
+            return ready
+        ranges = [(b.group, b.start, b.end, ready_fn(b)) for b in order]
+        # zero-width gaps are impossible (buckets tile each group), but a group with no bucket would be missed
+        covered = {id(b.group) for b in self.buckets}
+        for g in self.flat:
+            if id(g) not in covered:
+                ranges.append((g, 0, g.numel, lambda: None))
+        out = opt.step(grad_scale=self.grad_scale, zero_grad=zero_grad, ranges=ranges)
+        for es in estreams:
+            torch.cuda.current_stream(es.device).wait_stream(es)
+        self._reset()
+        return out
 
     def set_comm(self, on):
         """Turn the gradient collectives off (on=False: every rank steps on its own gradients) or back on.

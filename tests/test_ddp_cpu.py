@@ -186,3 +186,62 @@ def test_allreduce_bw_tool_gloo(tmp_path):
     rows = [_json.loads(line) for line in out.read_text().splitlines()]
     assert len(rows) >= 7 and all(x["n_ranks"] == 2 and x["us"] > 0 and x["busbw_GBs"] > 0 for x in rows)
     assert rows[-1]["tag"].startswith("resnet50_bucket")
+
+
+def _rank_step(rank, world, port, q):
+    """DataParallel.step (apply per bucket as each all-reduce lands) == finish() + opt.step(), bit for bit, over
+    two steps with momentum (several buckets, the fp32 and compute groups)."""
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import dtg  # noqa: F401
+        from dtg import ops
+        from dtg.optim import FusedAdam, FusedSGD
+        from dtg.parallel import DataParallel, FlatParams, comm
+        comm.init("gloo")
+        for Opt in (FusedSGD, FusedAdam):
+            runs = []
+            for mode in ("step", "finish"):
+                torch.manual_seed(0)
+                model = _mlp()
+                flat = FlatParams(model, compute_dtype=torch.float32)
+                dp = DataParallel(flat, bucket_mb=0.001)
+                assert len(dp.buckets) > 2
+                dp.broadcast_parameters(0)
+                opt = Opt(flat, lr=0.05)
+                g = torch.Generator().manual_seed(1 + rank)
+                for _ in range(2):
+                    x = torch.randn(8, 16, generator=g)
+                    y = torch.randint(0, 4, (8,), generator=g)
+                    ops.softmax_cross_entropy(model(x), y).backward()
+                    if mode == "step":
+                        dp.step(opt)
+                    else:
+                        dp.finish()
+                        opt.step(grad_scale=dp.grad_scale)
+                runs.append([p.detach().clone() for p in model.parameters()] +
+                            [grp.master.clone() for grp in flat])
+                dp.remove_hooks()
+            assert all(torch.equal(a, b) for a, b in zip(*runs)), Opt.__name__
+        comm.shutdown()
+        q.put((rank, "ok"))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_dp_step_overlapped_apply_equals_finish_then_step():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_step, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: "ok", 1: "ok"}, res
