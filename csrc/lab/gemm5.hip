@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(256, 1) g5_kernel(const bf16_t* __restrict__ A
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);  // no LDS access moves across the raw barrier
 #pragma unroll
   for (int q = 0; q < TI + TJ; ++q) rd(smem, 0, q);
 
@@ -119,6 +120,7 @@ __global__ void __launch_bounds__(256, 1) g5_kernel(const bf16_t* __restrict__ A
         for (int j = 0; j < TJ; ++j) mfma(acc[i][j], fa[1][i], fb[1][j]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);  // no LDS access moves across the raw barrier
       if constexpr (more) {
 #pragma unroll
         for (int q = 0; q < TI + TJ; ++q) rd(nxt, 0, q);
@@ -329,6 +331,7 @@ __global__ void __launch_bounds__(256, 1) g5p_kernel(const bf16_t* __restrict__ 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);  // no LDS access moves across the raw barrier
 #pragma unroll
   for (int q = 0; q < TI + TJ; ++q) rd(smem, 0, q);
 
