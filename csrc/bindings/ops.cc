@@ -6,8 +6,6 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
-#include <vector>
-
 #include "dtg/kernels.h"
 
 namespace {
@@ -946,24 +944,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, pybind11::arg("seconds"), pybind11::arg("wgs") = 32, pybind11::arg("mode") = 0,
         pybind11::arg("scratch") = pybind11::none(), pybind11::arg("base") = 0, pybind11::arg("traffic_bytes") = 0,
         pybind11::arg("bucket") = pybind11::none(), pybind11::arg("factor") = 1.0);
-  m.def("cu_masked_stream", [](int64_t device, int64_t ncu) {
-    // a HIP stream whose workgroups may run only on `ncu` CUs spread evenly over the chip (hipExtStreamCreateWithCUMask;
-    // the side stream of parallel/overlap.py under DTG_SIDE_CUS): the weight gradients then cannot take more than
-    // that share of the CU slots from the main stream's critical path.  Returned as an integer handle for
-    // torch.cuda.ExternalStream; never destroyed (one per device and process).
-    c10::DeviceGuard dg(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
-    int cus = 0;
-    TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, (int)device) == hipSuccess, "CU count");
-    TORCH_CHECK(ncu >= 1 && ncu <= cus, "ncu in [1, CU count]");
-    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-    for (int64_t k = 0; k < ncu; ++k) {
-      const int cu = (int)(k * cus / ncu);
-      mask[cu / 32] |= 1u << (cu % 32);
-    }
-    hipStream_t st = nullptr;
-    TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) == hipSuccess, "CU-masked stream");
-    return (int64_t)(uintptr_t)st;
-  });
   m.def("hyper_tick", [](Tensor hyper) {
     check_hyper(hyper);
     c10::DeviceGuard dg(hyper.device());

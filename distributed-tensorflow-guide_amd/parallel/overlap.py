@@ -77,21 +77,11 @@ def set_enabled(on):
     _ON = bool(on)
 
 
-# DTG_SIDE_CUS=<n>: the side stream is a CU-masked HIP stream limited to n CUs spread over the chip (A/B runs: the
-# weight gradients then cannot take more than that share of the CU slots from the main stream's critical path)
-_SIDE_CUS = int(os.environ.get("DTG_SIDE_CUS", "0"))
-
-
 def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        if _SIDE_CUS > 0:
-            from ..ops._native import lib
-            s = torch.cuda.ExternalStream(lib().cu_masked_stream(idx, _SIDE_CUS), device=torch.device("cuda", idx))
-        else:
-            s = torch.cuda.Stream(device=idx, priority=_PRIO)
-        _side[idx] = s
+        s = _side[idx] = torch.cuda.Stream(device=idx, priority=_PRIO)
     return s
 
 
