@@ -1,7 +1,8 @@
 // PyTorch bindings of the GEMM / conv lab kernels (module dtg._lab, built only by tools/build_ext.py --only lab and
 // imported through dtg.ops._native.lab()): A/B candidates and negative results that are not part of the production
 // extension _C -- the 256x256 8-phase GEMMs (gemm8.hip), the forced tile table (gemm_forced*.hip), the direct 3x3
-// halo conv (conv_halo.hip) and the round-5 main-loop lab (gemm5.hip).
+// halo conv (conv_halo.hip), the round-5 main-loop lab (gemm5.hip) and the transposed fused BN dx +
+// weight gradient (bn_dxT_wgrad.hip).
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -13,6 +14,9 @@ namespace lab {
 int gemm5_bf16(const bf16_t* A, const bf16_t* B, bf16_t* C, int M, int N, int K, int sched, hipStream_t st);
 int gemm5p_bf16(const bf16_t* A, const bf16_t* B, void* C, int c_bf16, int M, int N, int K, const float* bias, int act,
                 void* aux, int aux_mode, hipStream_t st, int grid);
+int bn_dxT_wgrad_slabs(int C, int CI);
+bool bn_dxT_wgrad(const bf16_t* dp, const bf16_t* x, const float* coef, bf16_t* dx, const bf16_t* act,
+                  long long ldact, float* wgrad, float* slabs, long long M, int C, int CI, hipStream_t st);
 }  // namespace lab
 }  // namespace dtg
 
@@ -23,6 +27,28 @@ using dtg::bf16_t;
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 const bf16_t* cbfp(const Tensor& t) { return reinterpret_cast<const bf16_t*>(t.data_ptr()); }
 bf16_t* bfp(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+
+// BN1 dx pass + conv1 weight gradient (bn_dxT_wgrad.hip): dx = a * dp + bx * x + c per channel (coef = [a, bx, c],
+// fp32 [3 C]), wgrad (fp32 [C, CI]) += dx^T act; returns dx.  C x CI = 64 x 256, 128 x 256 or 128 x 512.
+Tensor bn_dxT_wgrad(Tensor dp, Tensor x, Tensor coef, Tensor act, Tensor wgrad) {
+  for (const Tensor* t : {&dp, &x, &act})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2, "bf16 [M, *]");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous(), "coef fp32");
+  TORCH_CHECK(wgrad.is_cuda() && wgrad.scalar_type() == at::kFloat && wgrad.is_contiguous(), "wgrad fp32");
+  const long long M = x.size(0);
+  const int C = (int)x.size(1), CI = (int)act.size(1);
+  TORCH_CHECK(dp.sizes() == x.sizes() && act.size(0) == M && coef.numel() == 3LL * C && wgrad.numel() == (long long)C * CI,
+              "shapes: dp, x [M, C], act [M, CI], coef [3 C], wgrad [C, CI]");
+  const int ns = dtg::lab::bn_dxT_wgrad_slabs(C, CI);
+  TORCH_CHECK(ns > 0, "C x CI = 64 x 256, 128 x 256 or 128 x 512");
+  c10::DeviceGuard dg(x.device());
+  auto dx = at::empty_like(x);
+  auto slabs = at::empty({(long long)ns * C * CI}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(dtg::lab::bn_dxT_wgrad(cbfp(dp), cbfp(x), coef.data_ptr<float>(), bfp(dx), cbfp(act), act.stride(0),
+                                     wgrad.data_ptr<float>(), slabs.data_ptr<float>(), M, C, CI, cur_stream()),
+              "rows: a multiple of 32, at least 2048");
+  return dx;
+}
 
 // out[M, N] = A[M, K] B[N, K]^T (bf16, contiguous); false if the shape is not one the kernel serves
 bool gemm5(Tensor A, Tensor B, Tensor out, int64_t sched) {
@@ -140,5 +166,7 @@ PYBIND11_MODULE(_lab, m) {
         pybind11::arg("b_kc"), pybind11::arg("out"), pybind11::arg("alpha") = 1.0, pybind11::arg("beta") = 0.0,
         pybind11::arg("bias") = pybind11::none(), pybind11::arg("act") = 0, pybind11::arg("split_k") = 1,
         pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0);
+  m.def("bn_dxT_wgrad", &bn_dxT_wgrad, pybind11::arg("dp"), pybind11::arg("x"), pybind11::arg("coef"),
+        pybind11::arg("act"), pybind11::arg("wgrad"));
   m.def("conv_halo_fwd", &conv_halo_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("with_stats") = false);
 }

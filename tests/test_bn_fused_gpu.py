@@ -244,7 +244,7 @@ def test_mode3_packed_mask_bits():
     assert _rel(r[1][0], ref) < 1e-2
 
 
-# ---- BN apply + relu in the consumer GEMM's operand prologue (mfma_gemm.cuh XfA / XfB) ----------------
+# ---- BN backward dx pass fused with the producing conv's weight gradient (bn_dx_wgrad.hip) ---------------
 @pytest.mark.parametrize("dual", [False, True])
 @pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,CI", [(256, 64), (512, 128)])
@@ -254,9 +254,10 @@ def test_bn_dx_wgrad_fused(dual, gdtype, C, CI):
     bf16 gradient."""
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(3)
-    M = 8192
+    M = 8192 + 32 * 37  # not a multiple of the grid: workgroups end after different block counts
     L = lib()
-    assert L.bn_dx_wgrad_ok(M, C, CI) and not L.bn_dx_wgrad_ok(M, 2 * C, CI) and not L.bn_dx_wgrad_ok(M + 8, C, CI)
+    assert L.bn_dx_wgrad_ok(M, C, CI) and not L.bn_dx_wgrad_ok(M, C, CI // 2 + 8)
+    assert not L.bn_dx_wgrad_ok(M + 8, C, CI)
     dp = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
     x = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)
     x2 = torch.randn(M, C, generator=g).to(dev, torch.bfloat16)

@@ -3,7 +3,8 @@
 These are A/B candidates and negative results kept for the tools (tools/gemm_ab.py, gemm_sweep.py,
 epi_gemm_ab.py, conv_halo_ab.py, gemm5_ab.py): the 256x128 8-wave ring and the rest of the forced tile table
 (gemm_forced*.hip), the 256x256 8-phase GEMM and its persistent form (gemm8.hip), the direct 3x3 halo conv
-(conv_halo.hip) and the round-5 main-loop lab (gemm5.hip).  Marked ``lab`` (not ``gpu``): the production GPU
+(conv_halo.hip), the round-5 main-loop lab (gemm5.hip) and the transposed fused BN dx + weight gradient
+(bn_dxT_wgrad.hip).  Marked ``lab`` (not ``gpu``): the production GPU
 suite does not load the lab extension.  Run with ``python -m pytest tests/test_lab_gpu.py -m lab`` on a GPU box
 after ``python tools/build_ext.py --only lab``.
 """
@@ -146,3 +147,22 @@ def test_gemm5p_matches_fp32_reference(M, N, K, epi):
         assert _rel(out, g) < 2e-2
         g.backward(torch.ones_like(g))
         assert _rel(aux, pre.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C,CI", [(64, 256), (128, 256), (128, 512)])
+def test_bn_dxT_wgrad_matches_fp32_reference(C, CI):
+    """Transposed fused BN dx pass + weight gradient (csrc/lab/bn_dxT_wgrad.hip): dx = a dp + bx x + c per channel
+    against fp32 torch, and wgrad += dx^T act on the kernel's bf16 dx; the row count is not a multiple of the grid,
+    so the persistent workgroups end after different block counts."""
+    g = torch.Generator().manual_seed(7)
+    dev = torch.device("cuda")
+    M = 8192 + 32 * 37
+    dp, x = (torch.randn(M, C, generator=g).to(dev, torch.bfloat16) for _ in range(2))
+    act = torch.rand(M, CI, generator=g).to(dev, torch.bfloat16)
+    coef = torch.randn(3, C, generator=g).to(dev)
+    w0 = torch.randn(C, CI, generator=g).to(dev)
+    w = w0.clone()
+    dx = _lab().bn_dxT_wgrad(dp, x, coef.view(-1), act, w)
+    ref = coef[0] * dp.float() + coef[1] * x.float() + coef[2]
+    assert _rel(dx, ref) < 1e-2
+    assert _rel(w, w0 + dx.float().t() @ act.float()) < 1e-4

@@ -51,18 +51,19 @@ def test_gemm_gelu_aux_store_and_grad():
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 384, 192), (300, 200, 136)])
-def test_gemm_colsum_epilogue(M, N, K):
-    """Bias gradient fused into the dgrad GEMM epilogue (bn_epi.cuh mode 5): the stored output equals the
-    plain aux-mode-2 GEMM and colsum accumulates its column sums (full and ragged tiles)."""
+@pytest.mark.parametrize("aux_mode", [2, 4])
+def test_gemm_colsum_epilogue(M, N, K, aux_mode):
+    """Bias gradient fused into the dgrad GEMM epilogue (bn_epi.cuh mode 5): the stored output equals the plain
+    aux-mode-2 / 4 GEMM and colsum accumulates its column sums (full and ragged tiles)."""
     torch.manual_seed(2)
     dy = torch.randn(M, K, device=dev).bfloat16()
     w = torch.randn(K, N, device=dev).bfloat16() * 0.1
     pre = torch.randn(M, N, device=dev).bfloat16()
     d_ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    lib().gemm(dy, True, w, False, d_ref, 1.0, 0.0, None, 2, 0, pre, 2)
+    lib().gemm(dy, True, w, False, d_ref, 1.0, 0.0, None, 2, 0, pre, aux_mode)
     d = torch.empty_like(d_ref)
     cs = torch.full((N,), 0.5, device=dev)  # accumulates onto what is there
-    lib().gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, 2, colsum=cs)
+    lib().gemm(dy, True, w, False, d, 1.0, 0.0, None, 2, 0, pre, aux_mode, colsum=cs)
     assert torch.equal(d, d_ref)
     assert rel(cs - 0.5, d_ref.float().sum(0)) < 1e-4
 
