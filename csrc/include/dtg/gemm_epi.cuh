@@ -125,7 +125,12 @@ __device__ __forceinline__ void epi_store8_fast(const Epi& e, int m, int n, floa
 
 // epi_store8_fast plus bias / activation / aux (bf16, full aligned groups): the switches are
 // wave-uniform branches around whole 8-column loops, not per-element tests as in epi_store8.
-__device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, float (&v)[8]) {
+// PB: the bias of these 8 columns is already in registers (pb) -- a thread of the staged epilogue keeps one
+// column group for the whole tile, so the caller loads it once instead of once per group: loaded here, every
+// group waited for its own bias load (BERT FFN1 forward 155 -> 178 us with the bias, tools/epi_decomp.py)
+template <bool PB = false>
+__device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, float (&v)[8],
+                                                    const float* pb = nullptr) {
   const long long off = (long long)m * e.ldc + n;
   bf16_t* p = (bf16_t*)e.C + off;
   if (e.beta != 0.f) {
@@ -139,7 +144,12 @@ __device__ __forceinline__ void epi_store8_fast_act(const Epi& e, int m, int n, 
   }
   if (e.bias) {
     float b[8];
-    load8_f32(e.bias + n, b);
+    if constexpr (PB) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = pb[k];
+    } else {
+      load8_f32(e.bias + n, b);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] += b[k];
   }

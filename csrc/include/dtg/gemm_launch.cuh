@@ -73,7 +73,12 @@ __global__ void __launch_bounds__(CF::NTH, CF::NW == 4 ? 2 : 1) gemm_kernel(SA s
       auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast(e, m, n, v); };
       epilogue_staged<CF, decltype(op), FULL>(smem, acc, bm0, bn0, M, N, op);
     } else {
-      auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast_act(e, m, n, v); };
+      // a thread's 8-column group is the same in every pass of epilogue_staged: its bias is loaded once
+      static_assert(CF::NTH % (CF::BN / 8) == 0, "fixed column group per thread");
+      float pb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int nb = bn0 + (int)(threadIdx.x % (CF::BN / 8)) * 8;
+      if (e.bias && nb < N) load8_f32(e.bias + nb, pb);
+      auto op = [&](int m, int n, float (&v)[8]) { epi_store8_fast_act<true>(e, m, n, v, pb); };
       epilogue_staged<CF, decltype(op), FULL>(smem, acc, bm0, bn0, M, N, op);
     }
   } else {
