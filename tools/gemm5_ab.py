@@ -51,8 +51,10 @@ def main():
             # the BERT FFN1 forward epilogue: + bias, GELU, GELU'(pre) saved for the backward (dtg), or not (blas)
             "g5p_gelu": lambda: lab.gemm5p(A, B, outs["g5p_gelu"], bias, 2, aux["g5p_gelu"], 3),
             "dtg_gelu": lambda: L.gemm(A, True, B, True, outs["dtg_gelu"], 1.0, 0.0, bias, 2, 0, aux["dtg_gelu"], 3),
-            "blas_gelu": lambda: outs["blas_gelu"].copy_(torch._addmm_activation(bias.bfloat16(), A, B.t(),
-                                                                                  use_gelu=True)),
+            # (hipBLASLt's fused bias + GELU kernel; the result is a fresh tensor from the caching allocator -- an
+            # earlier version copied it into outs["blas_gelu"], which added a 201 MB copy to hipBLASLt's time)
+            "blas_gelu": lambda: outs.__setitem__("blas_gelu", torch._addmm_activation(bias.bfloat16(), A, B.t(),
+                                                                                        use_gelu=True)),
         }
         rows = torch.randint(0, M, (64,), device=dev)
         ref = A[rows].float() @ B.float().t()
