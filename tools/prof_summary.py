@@ -13,16 +13,34 @@ import csv
 import re
 
 
+def _targs(name, start):
+    """Top-level template arguments of the template whose '<' is at name[start]."""
+    args, depth, cur = [], 0, ""
+    for ch in name[start + 1:]:
+        if ch in "<(":
+            depth += 1
+        elif ch in ">)":
+            if depth == 0:
+                args.append(cur.strip())
+                return args
+            depth -= 1
+        if ch == "," and depth == 0:
+            args.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    return args
+
+
 def short(name):
     m = re.search(r"dtg::(\w+?)_kernel", name) or re.search(r"dtg::(\w+)", name)
     if m:
         base = m.group(1)
-        c = re.search(r"Cfg<(\d+), (\d+), (\d+), (\d+)(?:, (\d+))?>", name)
-        mode = re.search(r"Cfg<[^>]*>, (?:true|false), (?:true|false), [^,]+, [^,]+, (\d)", name)
-        if c:
-            base += f" {c.group(1)}x{c.group(2)}s{c.group(3)}"
-        if mode and mode.group(1) != "0":
-            base += f" bn{mode.group(1)}"
+        if base == "gemm" and "gemm_kernel<" in name:
+            # gemm_kernel<Cfg, AKC, BKC, SA, SB, BNMODE, FAST, BNPF>: the BN-epilogue mode tells the classes apart
+            a = _targs(name, name.index("gemm_kernel<") + len("gemm_kernel"))
+            if len(a) > 5 and a[5].isdigit() and a[5] != "0":
+                base += f" bn{a[5]}"
         return base
     return name[:48]
 
