@@ -197,6 +197,17 @@ def main(argv=None):
         # warmup = eager steps on a side stream + the capture; the rest of the warmup replays
         step = GraphedStep(step, warmup=min(2, max(a.warmup - 1, 1)))
     main_prio = os.environ.get("DTG_MAIN_PRIO")
+    if (main_prio is None and a.model == "bert" and world == 1 and os.environ.get("DTG_DDP_FORCE") != "1"
+            and "DTG_SIDE_PRIO" not in os.environ):
+        # BERT on one rank (no collective stream): the main stream (data gradients, LayerNorm, attention -- the
+        # critical path) on the high-priority queue and the weight-gradient side stream at normal priority, so
+        # the side stream's compute-bound GEMMs fill in around the main stream instead of taking CUs from it:
+        # 9,466 vs 9,345 seq/s (profiles/r05_stream_prio/ab_bert_prio.log).  ResNet-50 measured the opposite
+        # (its side stream must keep pace with a memory-bound main stream), and with ranks > 1 the process
+        # group's high-priority stream needs its own queue, so both keep the default order.
+        from dtg.parallel import overlap as _ov
+        _ov.set_side_priority(0)
+        main_prio = "-1"
     if main_prio is not None and device.type == "cuda" and not use_graph:
         # the whole step on a stream of this priority (A/B of the main / side stream priorities, DTG_SIDE_PRIO)
         ms = torch.cuda.Stream(device=device, priority=int(main_prio))

@@ -77,6 +77,12 @@ def set_enabled(on):
     _ON = bool(on)
 
 
+def set_side_priority(prio):
+    """Priority of the side streams created from now on (bench.py: BERT on one rank, see there)."""
+    global _PRIO
+    _PRIO = int(prio)
+
+
 def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
