@@ -438,7 +438,7 @@ static bool conv_skinny(int n) { return n <= 64; }
 // conv_set_stages() overrides it per pass (fwd, dgrad, wgrad) for A/B tools (tools/conv_sweep.sh).
 // Default (measured, profiles/r01_tiles): one stage, except fwd/dgrad grids shorter than 512
 // 128x128 tiles with a reduction of >= 2048 (the 7x7 / 512-channel layers), which keep the 2-deep ring.
-static int g_conv_stages[3] = {-1, -1, -1};
+static int g_conv_stages[4] = {-1, -1, -1, -1};  // fwd, dgrad, wgrad, 8-channel (stem) fwd
 static int conv_stages(int which, long long M = 0, int N = 0, int Kred = 0) {
   if (g_conv_stages[which] > 0) return g_conv_stages[which];
   if (which == 2) return 1;
@@ -447,7 +447,7 @@ static int conv_stages(int which, long long M = 0, int N = 0, int Kred = 0) {
 }
 // schedule code: 1 = single LDS stage, 2 = two-stage ring, 3 = single stage, register-pipelined (Cfg RP)
 void conv_set_stages(int which, int stages) {  // 0 restores the measured default
-  if (which >= 0 && which < 3) g_conv_stages[which] = stages >= 1 && stages <= 3 ? stages : -1;
+  if (which >= 0 && which < 4) g_conv_stages[which] = stages >= 1 && stages <= 3 ? stages : -1;
 }
 
 // Output tile forced per pass (fwd, dgrad) for A/B tools (conv_force_tile; tools/conv_tile_ab.py): 0 = the
@@ -500,10 +500,18 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
 }
 
 // 8-channel input (the stem, zero padded 3 -> 8); w is [K][Kp], Kp = ceil64(R*S*8), (r, s, c) order
+bool stem_conv_stream_bn(const bf16_t* x8, const bf16_t* w8, bf16_t* y, int N, int Hp, int Wp2, int P, int Q,
+                         float* part, hipStream_t st);
+
 void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int K, int R, int S, int stride,
                  int pad, hipStream_t st, const BnEpi& bn, int stride_w) {
   ConvGeom G = make_geom(N, H, W, 8, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q;
+  // ResNet's pixel-pair stem (64 channels, 7 x 4 taps = K 256 padded, (2, 1) stride, padding already in x): the
+  // streaming form (gemm_expand.hip)
+  if (bn.mode == 1 && K == 64 && R == 7 && S == 4 && stride == 2 && G.sw == 1 && pad == 0 &&
+      stem_conv_stream_bn(x, w, y, N, H, W, G.P, G.Q, bn.part, st))
+    return;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};
   auto run = [&](auto cf) {
     using CF = decltype(cf);
@@ -511,8 +519,9 @@ void conv_fwd_c8(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int 
     if (bn.mode == 1) { conv_fwd_kernel<CF, 1, true><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
     else { conv_fwd_kernel<CF, 0, true><<<tm * tn, CF::NTH, 0, st>>>(G, x, w, e, tn, bn); DTG_LAUNCH_CHECK(); }
   };
-  if (conv_skinny(K)) run(Cfg<256, 64, 1>());
-  else run(Cfg<128, 128, 1>());
+  const int sc = g_conv_stages[3] > 0 ? g_conv_stages[3] : 1;
+  if (conv_skinny(K)) run_sched<256, 64>(sc, run);
+  else run_sched<128, 128>(sc, run);
 }
 
 // 128x128 data gradients: where the default picks the 2-stage ring (short grid, long K: the 7x7 3x3

@@ -185,6 +185,139 @@ int expand_grid(int nslice) {
   return G > 0 ? G : mult;
 }
 
+// ---- the ResNet stem conv as a streaming GEMM ------------------------------------------------------------
+// The stem's 7x7/2 conv on pixel pairs (ops/conv.py stem_pairs: x8 [N, Hp, Wp/2, 8], 4 channels x 2 pixels per
+// 16-B chunk, a (2, 1)-stride conv with R = 7 rows x S2 = 4 pair-columns = 28 taps, zero-padded to K = 256) has the
+// shape of the expand GEMMs above: a short reduction into a write-bound output (12.8M pixels x 64 channels =
+// 1.64 GB at batch 1024).  The tiled implicit GEMM (conv_fwd_c8, 256x64 tiles, 4 K-steps each) spent 820 us on
+// it, twice its HBM time: every 256-row tile paid a pipeline fill and a staged epilogue with a block reduction of
+// the BN statistics.  Here, as in gemm_expand_bn_kernel: persistent workgroups, all 64 x 256 weights in registers
+// (wave w holds every column: 4 n-tiles x 8 k-steps, fed permuted), 64-row blocks of the gathered input through a
+// 3-deep LDS-DMA ring (each lane's DMA source address is the gather), wave w computes m-tile w of each block and
+// stores 2 x 16 B per lane straight from the MFMA registers, statistics in registers for the whole kernel.
+struct StemStreamGeom {
+  int Hp, Wp2, P, Q;
+  FastDiv fPQ, fQ;
+};
+
+__global__ void __launch_bounds__(256, 2) stem_stream_bn_kernel(const bf16_t* __restrict__ x8,
+                                                                 const bf16_t* __restrict__ W,
+                                                                 bf16_t* __restrict__ C, float* __restrict__ part,
+                                                                 StemStreamGeom sg, int nblocks) {
+  constexpr int K = 256, KS = K / 32, KH = K / 64, N = 64;
+  constexpr int BLK = kXR * K * 2;          // 32 KB: one 64-row block, [KH][64 rows][64 k] KC images
+  constexpr int D = KH * 2;                 // LDS-DMA instructions per lane per block
+  constexpr int T = 2;                      // 16-B stores per lane per block (one m-tile per wave)
+  constexpr int TAPS = 28;                  // 7 rows x 4 pair-columns; taps 28..31 read the zero page
+  constexpr int RING = 2;                   // LDS slots (2 x 32 KB: two workgroups per CU)
+  __shared__ __attribute__((aligned(16))) char smem_raw[RING * BLK];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int base = xcd_remap(blockIdx.x, G);  // consecutive logical ids (and so neighbouring blocks) share an XCD
+  const int my = base < nblocks ? (nblocks - base + G - 1) / G : 0;
+  if (my == 0) return;
+  const int q = lane & 15, g = lane >> 4;
+
+  v8bf wf[4][KS];  // every output column: n-tile j, fed permuted (see gemm_expand_bn_kernel)
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int n = 32 * (j >> 1) + 8 * (q >> 2) + 4 * (j & 1) + (q & 3);
+      wf[j][ks] = *reinterpret_cast<const v8bf*>(W + (long long)n * K + ks * 32 + 8 * g);
+    }
+
+  // block of iteration it = logical block base + it G; past the last block the last one is loaded again (never
+  // read), so every iteration issues exactly D DMA instructions and the counted waits stay uniform
+  auto stage = [&](int it) {
+    const int rb = base + (it < my ? it : my - 1) * G;
+    lds_char* dst = smem + (it % RING) * BLK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r0 = (wave * 2 + i) * 8, r = r0 + (lane >> 3);
+      uint32_t n, pq, p, qq;
+      sg.fPQ.divmod((uint32_t)(rb * kXR + r), n, pq);
+      sg.fQ.divmod(pq, p, qq);
+      const bf16_t* rowp = x8 + (((long long)n * sg.Hp + 2 * (int)p) * sg.Wp2 + (int)qq) * 8;
+#pragma unroll
+      for (int h = 0; h < KH; ++h) {
+        const int t = 8 * h + ((lane & 7) ^ (r & 7));  // the tap whose chunk belongs at this lane's LDS position
+        const void* src = sel(t < TAPS, rowp + ((t >> 2) * sg.Wp2 + (t & 3)) * 8);
+        __builtin_amdgcn_global_load_lds(src, (lds_void*)(dst + h * kXR * 128 + r0 * 128), 16, 0, 0);
+      }
+    }
+  };
+
+  float s[16], sq[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) s[c] = sq[c] = 0.f;
+  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  for (int it = 0; it < my; ++it) {
+    // block `it` landed once only the stores of block it-1 (issued after its DMA) can still be in flight; the other
+    // workgroup of the CU hides this one's DMA latency (a 3-slot ring at one workgroup per CU measured the same)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T) : "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's part of block `it` is in LDS; the slot of block it-1 is free
+    __builtin_amdgcn_sched_barrier(0);
+    stage(it + RING - 1);
+    const lds_char* ta = smem + (it % RING) * BLK;
+    const long long row0 = (long long)(base + it * G) * kXR;
+    v8bf af[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) af[ks] = frag_kc(ta + (ks >> 1) * kXR * 128, 16 * wave, ks & 1, lane);
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][0], af[0], zero4, 0, 0, 0);
+#pragma unroll
+    for (int ks = 1; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][ks], af[ks], acc[j], 0, 0, 0);
+    u32x4v w0, w1;
+    w0.x = pack_bf2(acc[0][0], acc[0][1]);
+    w0.y = pack_bf2(acc[0][2], acc[0][3]);
+    w0.z = pack_bf2(acc[1][0], acc[1][1]);
+    w0.w = pack_bf2(acc[1][2], acc[1][3]);
+    w1.x = pack_bf2(acc[2][0], acc[2][1]);
+    w1.y = pack_bf2(acc[2][2], acc[2][3]);
+    w1.z = pack_bf2(acc[3][0], acc[3][1]);
+    w1.w = pack_bf2(acc[3][2], acc[3][3]);
+    const uint32_t wd[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {  // statistics of what the BN pass will read (the rounded values)
+      const float lo = __uint_as_float(wd[c] << 16), hi = __uint_as_float(wd[c] & 0xffff0000u);
+      s[2 * c] += lo;
+      s[2 * c + 1] += hi;
+      sq[2 * c] = fmaf(lo, lo, sq[2 * c]);
+      sq[2 * c + 1] = fmaf(hi, hi, sq[2 * c + 1]);
+    }
+    bf16_t* dst = C + (row0 + 16 * wave + q) * N + 8 * g;
+    *reinterpret_cast<u32x4v*>(dst) = w0;
+    *reinterpret_cast<u32x4v*>(dst + 32) = w1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (dummy) DMAs land before the LDS is released
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s[c] += __shfl_xor(s[c], o, 64);
+      sq[c] += __shfl_xor(sq[c], o, 64);
+    }
+  }
+  if (q == 0) {
+    float* pp = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * N + 8 * g;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {  // value c: column 8 g + c (c < 8), 32 + 8 g + c - 8 (c >= 8)
+      const int off = c < 8 ? c : 24 + c;
+      atomicAdd(pp + off, s[c]);
+      atomicAdd(pp + N + off, sq[c]);
+    }
+  }
+}
+
 }  // namespace
 
 // false (nothing launched): not a shape this kernel serves, the caller takes the tiled path
@@ -208,6 +341,39 @@ bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long l
     else if (variant == 2) launch(gemm_expand_bn_kernel<128, false, 2>, expand_grid<128, false, 2>(nslice));
     else launch(gemm_expand_bn_kernel<128, false, 0>, expand_grid<128, false, 0>(nslice));
   }
+  DTG_LAUNCH_CHECK();
+  return true;
+}
+
+// The stem conv of ResNet (pixel-pair form: x8 [N, Hp, Wp2, 8], w8 [64][256], (2, 1) stride, P x Q output) with the
+// BN statistics into part (kBnStatSlots x 2 x 64, zeroed); false if the geometry is not that one
+static int g_stem_stream = 1;
+void stem_stream_set(int on) { g_stem_stream = on; }
+
+bool stem_conv_stream_bn(const bf16_t* x8, const bf16_t* w8, bf16_t* y, int N, int Hp, int Wp2, int P, int Q,
+                         float* part, hipStream_t st) {
+  if (!g_stem_stream) return false;
+  const long long M = (long long)N * P * Q;
+  if (M % kXR || M / kXR > (1LL << 30) || (long long)N * Hp * Wp2 * 8 >= (1LL << 31)) return false;
+  if (2 * (P - 1) + 7 > Hp || (Q - 1) + 4 > Wp2) return false;  // every tap inside the padded input
+  StemStreamGeom sg;
+  sg.Hp = Hp;
+  sg.Wp2 = Wp2;
+  sg.P = P;
+  sg.Q = Q;
+  sg.fPQ = FastDiv((uint32_t)(P * Q));
+  sg.fQ = FastDiv((uint32_t)Q);
+  static int G = 0;
+  if (G == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    DTG_HIP_CHECK(hipGetDevice(&dev));
+    DTG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DTG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stem_stream_bn_kernel, 256, 0));
+    G = cus * (per_cu < 1 ? 1 : per_cu);
+    G -= G % 8;
+    if (G < 8) G = 8;
+  }
+  hipLaunchKernelGGL(stem_stream_bn_kernel, dim3(G), dim3(256), 0, st, x8, w8, y, part, sg, (int)(M / kXR));
   DTG_LAUNCH_CHECK();
   return true;
 }

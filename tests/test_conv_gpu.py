@@ -124,3 +124,33 @@ def test_stem_pack_pairs_matches_pad(N, C, H, W, pad, S):
     assert torch.equal(wgot.cpu(), wref)
 
 
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_stem_stream_conv_matches_tiled(N):
+    """The streaming stem conv (gemm_expand.hip stem_stream_bn_kernel: persistent workgroups, all weights in
+    registers, gathered 64-row blocks through a 3-deep LDS-DMA ring) equals the tiled implicit GEMM on ResNet's
+    pixel-pair stem at 224 x 224 (fewer blocks than workgroups at N = 1), output and BN statistics, and the fp32
+    conv."""
+    from dtg.ops.conv import stem_pairs
+    from dtg.ops._native import lib
+    L = lib()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(N, 3, 224, 224, generator=g).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(DEV, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x8, w8, (rk, sk) = stem_pairs(x, w, 2, 3)
+    out = []
+    for on in (0, 1):
+        L.stem_stream_set(on)
+        try:
+            y, part = L.conv_fwd_c8(x8, w8, rk, sk, 2, 0, True, stride_w=1)
+        finally:
+            L.stem_stream_set(1)
+        out.append((y.float(), part.view(-1, 2, 64).sum(0)))
+    (yt, pt), (ys, ps) = out
+    assert _rel(ys, yt) < 1e-3
+    assert _rel(ps[0], pt[0]) < 1e-3 and _rel(ps[1], pt[1]) < 1e-3
+    ref = F.conv2d(x.float(), w.float(), None, 2, 3).permute(0, 2, 3, 1)
+    assert _rel(ys.view_as(ref), ref) < 1e-2
+    yf = ys.reshape(-1, 64)
+    assert _rel(ps[0], yf.sum(0)) < 1e-3

@@ -4,7 +4,8 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
 
     DTG_AB_BN_CFG=-1 python tools/bench_cfg.py [bench.py flags]     # BN-epilogue GEMMs without the expand kernel
     DTG_AB_SET=models.resnet_fused._DXW=0 python tools/bench_cfg.py  # a module switch (dtg.<module>.<name>=<int>)
-    DTG_AB_STAGES=0:2,1:3 python tools/bench_cfg.py   # conv LDS schedules per pass (0 fwd, 1 dgrad, 2 wgrad)
+    DTG_AB_STAGES=0:2,1:3 python tools/bench_cfg.py   # conv LDS schedules per pass (0 fwd, 1 dgrad, 2 wgrad, 3 stem)
+    DTG_AB_STEM_STREAM=0 python tools/bench_cfg.py    # the tiled stem conv instead of the streaming one
 """
 import os
 import runpy
@@ -16,6 +17,8 @@ sys.path.insert(0, ROOT)
 import dtg  # noqa: E402,F401
 from dtg.ops._native import lib  # noqa: E402
 
+if os.environ.get("DTG_AB_STEM_STREAM"):  # 0: the tiled stem conv instead of the streaming one
+    lib().stem_stream_set(int(os.environ["DTG_AB_STEM_STREAM"]))
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
