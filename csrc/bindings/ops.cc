@@ -580,8 +580,7 @@ std::tuple<Tensor, Tensor> conv_fwd_bn(Tensor x, Tensor w, int64_t stride, int64
   c10::DeviceGuard dg(x.device());
   auto y = at::empty({N, P, Q, K}, x.options());
   auto part = bn_part(x, K, pooled);
-  // (The direct halo-tile conv for 3x3 / s1 / p1, 64 -> 64, was 16 % faster alone but no faster in the training
-  // step, profiles/r03_conv_l2: it lives in the lab extension, csrc/lab/conv_halo.hip.)
+  // (3x3 / s1 / p1, 64 -> 64: conv_fwd takes the direct halo-tile conv, csrc/kernels/conv_halo.hip)
   dtg::BnEpi bn;
   bn.part = part.data_ptr<float>();
   bn.mode = 1;

@@ -252,6 +252,10 @@ void col2im(const bf16_t* dcols, bf16_t* dx, int N, int H, int W, int C, int R, 
 // ---- implicit-GEMM convolution, NHWC (conv.hip) ------------------------------------------------
 // which: 0 fwd, 1 dgrad, 2 wgrad.  Strided dgrad runs one dense launch per residue class of dx.
 int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
+// direct 3x3 / s1 / p1 conv, 64 -> 64 channels, with the BN forward statistics into part (conv_halo.hip; conv_fwd
+// takes it for BnEpi mode 1 when conv3x3_halo_bn_ok)
+int conv3x3_halo_bn_ok(int C, int K, int H, int W);
+void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st);
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
               int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 // returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad

@@ -154,3 +154,21 @@ def test_stem_stream_conv_matches_tiled(N):
     assert _rel(ys.view_as(ref), ref) < 1e-2
     yf = ys.reshape(-1, 64)
     assert _rel(ps[0], yf.sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,H", [(3, 56), (2, 28), (2, 30)])
+def test_conv_fwd_bn_halo_64(N, H):
+    """conv_fwd_bn for ResNet's stage-1 3x3 (64 -> 64, stride 1, pad 1): H % 4 == 0 runs the direct halo-tile conv
+    (csrc/kernels/conv_halo.hip), H = 30 the implicit GEMM; output against the fp32 conv, the BN-statistics partials
+    against the stored output's column sums and sums of squares."""
+    from dtg.ops._native import lib
+    L = lib()
+    g = torch.Generator(device="cpu").manual_seed(21 + H)
+    x = torch.randn(N, H, H, 64, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    y, part = L.conv_fwd_bn(x, w, 1, 1)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert _rel(y, ref) < 1e-2
+    p = part.view(-1, 2, 64).sum(0)
+    yf = y.float().reshape(-1, 64)
+    assert _rel(p[0], yf.sum(0)) < 1e-3 and _rel(p[1], (yf * yf).sum(0)) < 1e-3
