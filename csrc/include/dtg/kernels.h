@@ -256,6 +256,10 @@ int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
 // takes it for BnEpi mode 1 when conv3x3_halo_bn_ok)
 int conv3x3_halo_bn_ok(int C, int K, int H, int W);
 void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st);
+// its data gradient with the BN-backward mode-3 epilogue (packed mask bits, beta 0); false if bn is not that form
+bool conv3x3_halo_bn_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dp, int N, int H, int W, const BnEpi& bn,
+                           hipStream_t st);
+void conv3x3_halo_dgrad_set(int on);  // (A/B tools) the halo data gradient on / off
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
               int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 // returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad

@@ -597,6 +597,10 @@ static int conv_dgrad_strided(const ConvGeom& G, const bf16_t* dy, const bf16_t*
 
 int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int W, int C, int K, int R, int S,
                int stride, int pad, float beta, hipStream_t st, const BnEpi& bn, const bf16_t* wT, int zero_rest) {
+  // 64 -> 64 3x3 / s1 / p1 with the BN-backward mode-3 epilogue (ResNet-50 stage 1): the direct halo-tile form
+  if (R == 3 && S == 3 && stride == 1 && pad == 1 && beta == 0.f && g_conv_tile[1] == 0 && g_conv_stages[1] <= 0 &&
+      conv3x3_halo_bn_ok(C, K, H, W) && conv3x3_halo_bn_dgrad(dy, w, dx, N, H, W, bn, st))
+    return 1;
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   if (stride != 1) return conv_dgrad_strided(G, dy, w, dx, beta, st, bn, zero_rest);
   const int M = N * H * W;

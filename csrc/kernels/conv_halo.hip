@@ -27,13 +27,25 @@ __device__ __forceinline__ int swz_off(int row, int chunk) { return row * 128 + 
 // after its run of bands (uniform loop bound).
 constexpr int kPF = 11;  // 16-byte halo chunks per thread: (kTH + 2) * (W + 2) * 8 <= 256 * kPF
 
-// part != nullptr: BatchNorm forward statistics of the stored (bf16) output, sum and sum of squares per
-// channel, kept in registers across the workgroup's bands and added once into part[blockIdx % kBnStatSlots]
-// (the conv_fwd_bn contract, kernels.h: BnEpi mode 1)
-template <bool STATS>
+// EPI 0 (forward): BatchNorm forward statistics of the stored (bf16) output, sum and sum of squares per channel,
+// kept in registers across the workgroup's bands and added once into part[blockIdx % kBnStatSlots] (the
+// conv_fwd_bn contract, kernels.h: BnEpi mode 1).
+// EPI 1 (data gradient of the same conv, BN-backward mode 3 epilogue): x is dy, the weights are staged flipped and
+// transposed (tap t of the dgrad correlation is w[k][8 - t][c], reduced over k), and each output element becomes
+// dp = relu-mask bit ? dx : 0 with the partials sum(dp), sum(dp * xhat) of the BN whose input is bn.x (the
+// conv_dgrad_bn contract: BnEpi mode 3 with packed mask bits, beta 0).
+struct HaloBwd {
+  const bf16_t* x;          // the BN input [M, 64] (xhat = (x - mean) * invstd)
+  const uint8_t* bits;      // relu mask [M, 8]
+  const float* mean;
+  const float* invstd;
+};
+
+template <int EPI>
 __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                              bf16_t* __restrict__ y, int N, int H, int W,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, HaloBwd hb) {
+  constexpr bool STATS = EPI == 0;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
   const int HW2 = W + 2, halo_px = (kTH + 2) * HW2, hbytes = halo_px * 128;
@@ -44,10 +56,25 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
   const int b0 = (int)((long long)blockIdx.x * total / gridDim.x);
   const int b1 = (int)((long long)(blockIdx.x + 1) * total / gridDim.x);
 
-  for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t = r*3 + s][k][c]
-    const int ch = i & 7, k = (i >> 3) & 63, t = i >> 9;
-    const u32x4v v = *reinterpret_cast<const u32x4v*>(w + ((long long)k * 9 + t) * kC + ch * 8);
-    *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(wt + t * 64 * 128 + swz_off(k, ch)) = v;
+  if constexpr (EPI == 0) {
+    for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t = r*3 + s][k][c]
+      const int ch = i & 7, k = (i >> 3) & 63, t = i >> 9;
+      const u32x4v v = *reinterpret_cast<const u32x4v*>(w + ((long long)k * 9 + t) * kC + ch * 8);
+      *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(wt + t * 64 * 128 + swz_off(k, ch)) = v;
+    }
+  } else {
+    for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t][c][k] = w[k][8 - t][c]: 8 c per load
+      const int cc = i & 7, k = (i >> 3) & 63, t = i >> 9;
+      const u32x4v v = *reinterpret_cast<const u32x4v*>(w + ((long long)k * 9 + (8 - t)) * kC + cc * 8);
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cc * 8 + e;
+        const uint16_t h16 = (uint16_t)(e & 1 ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xffffu);
+        *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wt + t * 64 * 128 + swz_off(c, k >> 3) +
+                                                                       (k & 7) * 2) = h16;
+      }
+    }
   }
   u32x4v pf[kPF];
   auto gload = [&](int band) {
@@ -86,6 +113,9 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     hbase[i] = oh * HW2 + ow;
   }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};  // channel j*16 + lane%16
+  float bs[8], bq[8];  // EPI 1: sum(dp), sum(dp * x) of channels 8 (lane & 7) + e over this lane's pixels
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = bq[e] = 0.f;
   int cur = 0;
   for (int band = b0; band < b1; ++band) {
     if (band + 1 < b1) gload(band + 1);
@@ -115,6 +145,19 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][i], b[s & 1][j], acc[i][j], 0, 0, 0);
     }
+    const int n_ = band / bands, oh0_ = (band - n_ * bands) * kTH;
+    const long long px0 = ((long long)n_ * H + oh0_) * W;
+    u32x4v xv[8];
+    uint32_t mb[8];
+    if constexpr (EPI == 1) {  // the epilogue's BN input and mask bits, in flight under the staging below
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int idx = k * 64 + lane, pr = idx >> 3, ch = idx & 7, p = wave * 64 + pr;
+        const long long o = px0 + (p < npx ? p : npx - 1);
+        xv[k] = *reinterpret_cast<const u32x4v*>(hb.x + o * kC + ch * 8);
+        mb[k] = hb.bits[o * (kC / 8) + ch];
+      }
+    }
     __syncthreads();  // every wave is done with hbuf[cur]: reuse it for the output staging
     lds_char* st = hbuf[cur] + wave * 64 * 128;
 #pragma unroll
@@ -133,14 +176,29 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
           }
         }
     __syncthreads();
-    const int n = band / bands, oh0 = (band - n * bands) * kTH;
-    const long long out0 = ((long long)n * H + oh0) * W;
+    const long long out0 = px0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int idx = k * 64 + lane, pr = idx >> 3, ch = idx & 7;
       const int p = wave * 64 + pr;
       if (p < npx) {
-        const u32x4v v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4v*>(st + pr * 128 + ch * 16);
+        u32x4v v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4v*>(st + pr * 128 + ch * 16);
+        if constexpr (EPI == 1) {  // dp = mask ? dx : 0 and the BN-backward partials (raw moment of x)
+          const uint32_t vd[4] = {v.x, v.y, v.z, v.w}, xd[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+          uint32_t od[4];
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const uint32_t lo_m = (mb[k] >> (2 * e2)) & 1u, hi_m = (mb[k] >> (2 * e2 + 1)) & 1u;
+            const uint32_t lo = lo_m ? (vd[e2] & 0xffffu) : 0u, hi = hi_m ? (vd[e2] & 0xffff0000u) : 0u;
+            od[e2] = lo | hi;
+            const float dl = __uint_as_float(lo << 16), dh = __uint_as_float(hi);
+            bs[2 * e2] += dl;
+            bs[2 * e2 + 1] += dh;
+            bq[2 * e2] = fmaf(dl, __uint_as_float(xd[e2] << 16), bq[2 * e2]);
+            bq[2 * e2 + 1] = fmaf(dh, __uint_as_float(xd[e2] & 0xffff0000u), bq[2 * e2 + 1]);
+          }
+          v.x = od[0]; v.y = od[1]; v.z = od[2]; v.w = od[3];
+        }
         *reinterpret_cast<u32x4v*>(y + (out0 + p) * kC + ch * 8) = v;
       }
     }
@@ -166,6 +224,24 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
       }
     }
   }
+  if constexpr (EPI == 1) {  // lanes sharing lane & 7 hold the same channels: fold, convert, one atomic each
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        bs[e] += __shfl_xor(bs[e], o);
+        bq[e] += __shfl_xor(bq[e], o);
+      }
+    if (lane < 8 && b0 < b1) {
+      float* slot = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * kC;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = lane * 8 + e;
+        atomicAdd(slot + c, bs[e]);
+        atomicAdd(slot + kC + c, hb.invstd[c] * (bq[e] - hb.mean[c] * bs[e]));  // sum(dp * xhat)
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -180,19 +256,43 @@ int conv3x3_halo_bn_ok(int C, int K, int H, int W) {
          halo_bn_lds(W) <= 160 * 1024;
 }
 
-void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st) {
+static int halo_cus() {
   static int n_cu = 0;
   if (!n_cu) {
-    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_pp_kernel<true>,
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_pp_kernel<0>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_pp_kernel<1>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     int dev = 0;
     DTG_HIP_CHECK(hipGetDevice(&dev));
     DTG_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  const int total = N * (H / kTH);
+  return n_cu;
+}
+
+void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st) {
+  const int n_cu = halo_cus(), total = N * (H / kTH);
   const dim3 grid(total < n_cu ? total : n_cu);
-  hipLaunchKernelGGL(conv3x3_halo_pp_kernel<true>, grid, dim3(256), halo_bn_lds(W), st, x, w, y, N, H, W, part);
+  hipLaunchKernelGGL(conv3x3_halo_pp_kernel<0>, grid, dim3(256), halo_bn_lds(W), st, x, w, y, N, H, W, part,
+                     HaloBwd{});
   DTG_LAUNCH_CHECK();
+}
+
+static int g_halo_dgrad = 1;
+void conv3x3_halo_dgrad_set(int on) { g_halo_dgrad = on; }  // 0 off, 1 on, > 1 on with a grid of that size
+
+bool conv3x3_halo_bn_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dp, int N, int H, int W, const BnEpi& bn,
+                           hipStream_t st) {
+  if (!g_halo_dgrad || bn.mode != 3 || !bn.maskbits || !bn.x || bn.x2 || bn.old_sub2 || !bn.mean || !bn.invstd)
+    return false;
+  // on > 1: a grid of that many workgroups (one per CU), leaving the rest of the chip to the side stream's wgrads
+  const int n_cu = g_halo_dgrad > 1 ? g_halo_dgrad : halo_cus(), total = N * (H / kTH);
+  halo_cus();
+  const dim3 grid(total < n_cu ? total : n_cu);
+  hipLaunchKernelGGL(conv3x3_halo_pp_kernel<1>, grid, dim3(256), halo_bn_lds(W), st, dy, w, dp, N, H, W, bn.part,
+                     HaloBwd{bn.x, bn.maskbits, bn.mean, bn.invstd});
+  DTG_LAUNCH_CHECK();
+  return true;
 }
 
 }  // namespace dtg

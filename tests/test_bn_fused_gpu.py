@@ -149,6 +149,38 @@ def test_conv_bn_fwd_and_dgrad_stats(C, K, H, R, st, pad):
         assert _rel(s3, sr) < 1e-2 and _rel(q3, qr) < 1e-2
 
 
+@pytest.mark.parametrize("N,H", [(2, 56), (3, 28)])
+def test_conv_dgrad_bn_halo_64(N, H):
+    """conv_dgrad_bn with packed mask bits for ResNet's stage-1 3x3 (64 -> 64, s1, p1) runs the direct halo-tile
+    data gradient (csrc/kernels/conv_halo.hip, EPI 1): against the fp32 reference and against the implicit-GEMM
+    dgrad (conv_halo_dgrad_set(0)) with the same epilogue."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(40 + H)
+    C = 64
+    L = lib()
+    w = (torch.randn(C, 3, 3, C, generator=g) * (9 * C) ** -0.5).to(dev, torch.bfloat16)
+    dy = torch.randn(N, H, H, C, generator=g).to(dev, torch.bfloat16)
+    xin = torch.randn(N * H * H, C, generator=g).to(dev, torch.bfloat16)
+    mean, inv, gamma, beta = _chan(C, dev, g)
+    bits = _pack_mask(xin, mean, inv, gamma, beta)
+    gref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2).float(),
+                                      padding=1).permute(0, 2, 3, 1).reshape(-1, C)
+    dpr, sr, qr = _bwd_ref(gref, xin, mean, inv, gamma, beta)
+    outs = []
+    for halo in (1, 0):
+        L.conv_halo_dgrad_set(halo)
+        try:
+            dp, part = L.conv_dgrad_bn(dy, w, H, H, 1, 1, xin, mean, inv, gamma, beta, bits=bits)
+        finally:
+            L.conv_halo_dgrad_set(1)
+        assert _rel(dp.view(-1, C), dpr) < 1e-2
+        s, q = _bn_stats(part, C)
+        assert _rel(s, sr) < 1e-2 and _rel(q, qr) < 1e-2
+        outs.append((dp.float(), s, q))
+    assert _rel(outs[0][0], outs[1][0]) < 5e-3
+    assert _rel(outs[0][1], outs[1][1]) < 5e-3 and _rel(outs[0][2], outs[1][2]) < 5e-3
+
+
 @pytest.mark.parametrize("res", [False, True])
 def test_bn_part_matches_unfused(res):
     """bn_fwd_part / bn_bwd_part (statistics from an epilogue) equal bn_fwd_train / bn_bwd."""

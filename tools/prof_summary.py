@@ -33,7 +33,8 @@ def _targs(name, start):
 
 
 def short(name):
-    m = re.search(r"dtg::(\w+?)_kernel", name) or re.search(r"dtg::(\w+)", name)
+    m = (re.search(r"dtg::(?:\(anonymous namespace\)::)?(\w+?)_kernel", name)
+         or re.search(r"dtg::(?:\(anonymous namespace\)::)?(\w+)", name))
     if m:
         base = m.group(1)
         if base == "gemm" and "gemm_kernel<" in name:
