@@ -260,6 +260,10 @@ void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int
 bool conv3x3_halo_bn_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dp, int N, int H, int W, const BnEpi& bn,
                            hipStream_t st);
 void conv3x3_halo_dgrad_set(int on);  // (A/B tools) the halo data gradient on / off
+// its weight gradient (W = 56): the split (= workgroups, one fp32 slab each) conv_wgrad uses, 0 if not this shape
+int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w);
+void conv3x3_halo_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int grid, int N, int H, hipStream_t st);
+void conv3x3_halo_wgrad_set(int on);  // (A/B tools) the halo weight gradient on / off
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
               int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 // returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad

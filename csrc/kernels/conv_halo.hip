@@ -244,6 +244,176 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
   }
 }
 
+
+// Weight gradient of the same conv, dW[k][r][s][c] = sum over pixels p of dy[p][k] * x[p + (r - 1, s - 1)][c]: a GEMM
+// 64 (k) x 576 (tap, c) reduced over pixels, so both operands are needed pixel-major -- exactly how NHWC stores them.
+// Each band stages its dy rows ([px][64 k]) and its x rows with the 1-pixel halo ONCE into LDS and every operand
+// fragment is a transposed read (ds_read_b64_tr_b16: 4 pixel rows x 16 channels per 16-lane group); a tap's B
+// fragment reads the halo rows of the shifted pixels, so x crosses L2 (kTH + 2) / kTH times instead of 9 times
+// through an im2col gather (conv.hip's implicit wgrad).  Persistent: one workgroup per CU walks a contiguous run of
+// bands, accumulating its 64 x 576 fp32 partial in registers (wave w: the column tiles 9w .. 9w + 8); the next
+// band's dy + halo are loaded into registers a few chunks per 32-pixel step and written to the other LDS buffer two
+// steps later, under this band's MFMAs.  One fp32 slab per workgroup, summed by the split-K reduce.
+// LDS images: 128-B rows, 16-B chunks XOR-swizzled by (row & 7) ^ 4 * ((row >> 3) & 1) (the two 4-row blocks a
+// 32-lane half reads, 8 rows apart, land in different banks).  The halo rows are 64 pixels apart (W + 2 <= 64), so
+// a fragment row's swizzle is a per-lane constant (A) or a per-lane table entry XOR one per-step bit (B), and every
+// read address is one VALU op (or none) instead of a swizzle evaluation: the first version spent ~2000 VALU
+// instructions per band on read addresses and ran the MFMA pipe at 24 %.
+__device__ __forceinline__ int wswz(int row, int chunk) {
+  return row * 128 + ((chunk ^ (row & 7) ^ ((row >> 1) & 4)) << 4);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) conv3x3_halo_wgrad_kernel(const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ dy,
+                                                                float* __restrict__ ws, int N, int H) {
+  static_assert(W % 8 == 0 && W + 2 <= 64, "8-pixel fragment groups inside an image row; 64-pixel halo pitch");
+  constexpr int HP = 64, hrows = kTH + 2, hbytes = hrows * HP * 128;
+  constexpr int npx = kTH * W, nst = npx / 32, dyrows = npx;
+  static_assert(npx % 32 == 0, "whole 32-pixel reduction steps");
+  constexpr int bufb = hbytes + dyrows * 128;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, q = (lane & 15) >> 2, pl = lane & 3;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bands = H / kTH, total = N * bands;
+  const int b0 = (int)((long long)blockIdx.x * total / gridDim.x);
+  const int b1 = (int)((long long)(blockIdx.x + 1) * total / gridDim.x);
+
+  // a band's halo (hrows x 64 pixels, columns past W + 1 unused) and dy rows as 16-byte chunks, kXP + kDP per
+  // thread; branch-free: every lane loads from a clamped in-bounds address and out-of-range chunks are zeroed at
+  // the LDS write (a load under a lane condition splits the code into blocks, and the compiler then drains every
+  // outstanding load at the join instead of counting them).  LDS-DMA is not used: the compiler drains in-flight
+  // DMA before the first LDS read of each step, which serialised the next band's loads with this band's MFMAs.
+  constexpr int kXP = hrows * HP * 8 / 256, kDP = (dyrows * 8 + 255) / 256, kCH = kXP + kDP;
+  auto cload = [&](int band, int ci, bool& ok) {
+    const int n = band / bands, oh0 = (band - n * bands) * kTH;
+    long long off;
+    if (ci < kXP) {
+      const int i = tid + ci * 256, r = i >> 3, ch = i & 7;
+      const int ih = oh0 - 1 + (r >> 6), iw = (r & 63) - 1;
+      ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      off = (((long long)n * H + (ok ? ih : oh0)) * W + (ok ? iw : 0)) * kC + ch * 8;
+    } else {
+      const int i = tid + (ci - kXP) * 256, r = i >> 3;
+      ok = r < npx;
+      off = (((long long)n * H + oh0) * W + (ok ? r : 0)) * kC + (i & 7) * 8;
+    }
+    return *reinterpret_cast<const u32x4v*>((ci < kXP ? x : dy) + off);
+  };
+  auto cstore = [&](lds_char* b, int ci, const u32x4v& v, bool ok) {
+    const u32x4v z = {0u, 0u, 0u, 0u}, w = ok ? v : z;
+    if (ci < kXP) {
+      const int i = tid + ci * 256;
+      *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(b + wswz(i >> 3, i & 7)) = w;
+    } else {
+      const int i = tid + (ci - kXP) * 256;
+      if (i < dyrows * 8)
+        *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(b + hbytes + wswz(i >> 3, i & 7)) = w;
+    }
+  };
+
+  // read-address tables.  A (dy image, rows 32 st + 8 g + q + 4 h): the swizzle of such a row is
+  // (q + 4h) ^ 4 (g & 1) for every step, so offA[h][i] + st * 4096 is the address.  B (halo, rows
+  // (32 st + 8 g) / W * 64 + (32 st + 8 g) % W + 4h + q + dr * 64 + ds): with w0 = (32 st + 8 g) % W a multiple of 8,
+  // the swizzle is sw(4h + q + ds) ^ 4 ((w0 >> 3) & 1), so the address is (offB[h][j] ^ (flip << 6)) + rowbase.
+  auto sw16 = [](int v) { return (v & 7) ^ ((v >> 1) & 4); };
+  int offA[2][4], offB[2][9];
+  const int sub = (pl & 1) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 8 * g + 4 * h + q, ch = (i * 16 + 4 * pl) >> 3;
+      offA[h][i] = hbytes + r * 128 + ((ch ^ sw16(r)) << 4) + sub;
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int jj = 9 * wave + j, t = jj >> 2, dr = t / 3, ds = t - dr * 3, ch = ((jj & 3) * 16 + 4 * pl) >> 3;
+      const int v = 4 * h + q + ds;
+      offB[h][j] = (dr * HP + v) * 128 + ((ch ^ sw16(v)) << 4) + sub;
+    }
+  }
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (b0 < b1) {
+#pragma unroll
+    for (int ci = 0; ci < kCH; ++ci) {
+      bool ok;
+      const u32x4v v = cload(b0, ci, ok);
+      cstore(smem, ci, v, ok);
+    }
+  }
+  __syncthreads();
+  // next band's chunks: kPS per step, loaded at step st and written to the other buffer two steps later
+  constexpr int kPS = (kCH + nst - 2) / (nst - 1), kSets = (kCH + kPS - 1) / kPS;
+  static_assert(kSets <= nst, "every chunk set is loaded within the band's steps");
+  u32x4v stg[kSets][kPS];
+  bool sok[kSets][kPS];
+  int cur = 0;
+  for (int band = b0; band < b1; ++band) {
+    const int nb = band + 1 < b1 ? band + 1 : band;  // the last band reloads itself into the unused buffer (no branch)
+    lds_char* other = smem + (cur ^ 1) * bufb;  // its last readers passed the previous barrier
+    const uint32_t buf = (uint32_t)(uintptr_t)(smem + cur * bufb);
+    v8bf a[4], b[9];
+#pragma unroll
+    for (int st = 0; st < nst; ++st) {
+      if (st < kSets) {
+#pragma unroll
+        for (int k = 0; k < kPS; ++k)
+          if (st * kPS + k < kCH) stg[st][k] = cload(nb, st * kPS + k, sok[st][k]);
+      }
+      {
+        const int pix = 32 * st + 8 * g, orow = pix / W, w0 = pix - orow * W;
+        uint32_t rb = buf + (uint32_t)(orow * HP + w0) * 128u, fl = (uint32_t)((w0 >> 3) & 1) << 6;
+        asm volatile("" : "+v"(rb), "+v"(fl));  // this step's addresses are computed in this step (not hoisted)
+        const uint32_t ab = buf + st * 4096;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[0][i]));
+          const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[1][i]));
+          a[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[0][j] ^ fl) + rb));
+          const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[1][j] ^ fl) + rb));
+          b[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if (st >= 2 && st - 2 < kSets) {
+#pragma unroll
+        for (int k = 0; k < kPS; ++k)
+          if ((st - 2) * kPS + k < kCH) cstore(other, (st - 2) * kPS + k, stg[st - 2][k], sok[st - 2][k]);
+      }
+    }
+#pragma unroll
+    for (int s2 = nst - 2; s2 < kSets; ++s2)
+#pragma unroll
+      for (int k = 0; k < kPS; ++k)
+        if (s2 * kPS + k < kCH) cstore(other, s2 * kPS + k, stg[s2][k], sok[s2][k]);
+    __syncthreads();  // next band visible; every wave is done reading this one before it is overwritten
+    cur ^= 1;
+  }
+  float* slab = ws + (long long)blockIdx.x * (kC * 9 * kC);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slab[(i * 16 + g * 4 + r) * (9 * kC) + (9 * wave + j) * 16 + (lane & 15)] = acc[i][j][r];
+}
+
 }  // namespace
 
 static size_t halo_bn_lds(int W) {
@@ -293,6 +463,34 @@ bool conv3x3_halo_bn_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dp, int N,
                      HaloBwd{bn.x, bn.maskbits, bn.mean, bn.invstd});
   DTG_LAUNCH_CHECK();
   return true;
+}
+
+// ---- weight gradient (conv_wgrad for 64 -> 64, 3x3 / s1 / p1, W = 56) ----
+constexpr int kWgW = 56;
+static size_t halo_wgrad_lds() {
+  constexpr int halo = (kTH + 2) * 64 * 128, dyb = kTH * kWgW * 128;
+  return 2 * (size_t)(halo + dyb);
+}
+static int g_halo_wgrad = 1;
+void conv3x3_halo_wgrad_set(int on) { g_halo_wgrad = on; }
+
+int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
+  if (!g_halo_wgrad || C != kC || K != kC || R != 3 || S != 3 || stride != 1 || pad != 1 ||
+      (stride_w != 0 && stride_w != 1) || W != kWgW || H % kTH != 0 || halo_wgrad_lds() > 160 * 1024)
+    return 0;
+  static int n_cu = 0;
+  if (!n_cu) {
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_wgrad_kernel<kWgW>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    n_cu = halo_cus();
+  }
+  const int total = N * (H / kTH);
+  return total < n_cu ? total : n_cu;
+}
+
+void conv3x3_halo_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int grid, int N, int H, hipStream_t st) {
+  hipLaunchKernelGGL(conv3x3_halo_wgrad_kernel<kWgW>, dim3(grid), dim3(256), halo_wgrad_lds(), st, x, dy, ws, N, H);
+  DTG_LAUNCH_CHECK();
 }
 
 }  // namespace dtg

@@ -172,3 +172,30 @@ def test_conv_fwd_bn_halo_64(N, H):
     p = part.view(-1, 2, 64).sum(0)
     yf = y.float().reshape(-1, 64)
     assert _rel(p[0], yf.sum(0)) < 1e-3 and _rel(p[1], (yf * yf).sum(0)) < 1e-3
+
+
+@pytest.mark.parametrize("N,beta,bf16_out", [(2, 0.0, False), (19, 1.0, False), (3, 0.0, True)])
+def test_conv_wgrad_halo_64(N, beta, bf16_out):
+    """conv_wgrad for ResNet's stage-1 3x3 (64 -> 64, s1, p1, 56x56) runs the persistent halo-tile weight gradient
+    (csrc/kernels/conv_halo.hip, one fp32 slab per workgroup + the split-K reduce): against the fp32 conv2d_weight and
+    the implicit-GEMM wgrad (conv_halo_wgrad_set(0)).  N = 19: 266 bands over 256 workgroups (some walk two);
+    beta = 1 accumulates into an existing gradient; bf16_out writes a bf16 dw."""
+    from dtg.ops._native import lib
+    L = lib()
+    g = torch.Generator(device="cpu").manual_seed(60 + N)
+    x = torch.randn(N, 56, 56, 64, generator=g).to(DEV, torch.bfloat16)
+    dy = torch.randn(N, 56, 56, 64, generator=g).to(DEV, torch.bfloat16)
+    dw0 = torch.randn(64, 3, 3, 64, generator=g).to(DEV)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (64, 64, 3, 3), dy.float().permute(0, 3, 1, 2),
+                                      padding=1).permute(0, 2, 3, 1) + beta * dw0
+    outs = []
+    for halo in (1, 0):
+        dw = dw0.clone().to(torch.bfloat16 if bf16_out else torch.float32)
+        L.conv_halo_wgrad_set(halo)
+        try:
+            L.conv_wgrad(dy, x, dw, beta, 1, 1)
+        finally:
+            L.conv_halo_wgrad_set(1)
+        assert _rel(dw, ref) < (1e-2 if bf16_out else 2e-3)
+        outs.append(dw.float())
+    assert _rel(outs[0], outs[1]) < (1e-2 if bf16_out else 2e-3)

@@ -8,6 +8,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
     DTG_AB_STEM_STREAM=0 python tools/bench_cfg.py    # the tiled stem conv instead of the streaming one
     DTG_AB_HALO=1 python tools/bench_cfg.py           # the lab's halo conv for ResNet's stage-1 3x3 forward
     DTG_AB_HALO_DGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 dgrad instead of the halo one
+    DTG_AB_HALO_WGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 wgrad instead of the halo one
 """
 import os
 import runpy
@@ -34,6 +35,8 @@ if os.environ.get("DTG_AB_STEM_STREAM"):  # 0: the tiled stem conv instead of th
     lib().stem_stream_set(int(os.environ["DTG_AB_STEM_STREAM"]))
 if os.environ.get("DTG_AB_HALO_DGRAD"):  # 0: the implicit-GEMM dgrad for the stage-1 3x3 (conv_halo.hip EPI 1)
     lib().conv_halo_dgrad_set(int(os.environ["DTG_AB_HALO_DGRAD"]))
+if os.environ.get("DTG_AB_HALO_WGRAD"):  # 0: the implicit-GEMM wgrad for the stage-1 3x3 (conv_halo.hip)
+    lib().conv_halo_wgrad_set(int(os.environ["DTG_AB_HALO_WGRAD"]))
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages

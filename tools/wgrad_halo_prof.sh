@@ -1,0 +1,9 @@
+#!/bin/bash
+# kernel-trace stats and one PMC pass of the stage-1 halo weight gradient (tools/wgrad3_bench.py --stages 1)
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/wgh
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $R/tools/wgrad3_bench.py --stages 1 --targets 256 --iters 10 > $OUT/kt.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/p1 -o run -- python3 $R/tools/wgrad3_bench.py --stages 1 --targets 256 --iters 3 > $OUT/p1.log 2>&1 || exit $?
