@@ -18,6 +18,7 @@ namespace {
 
 constexpr int kTH = 4, kC = 64;
 
+
 __device__ __forceinline__ int swz_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
 // Persistent, software-pipelined form: one workgroup per CU keeps all 9 weight taps resident in LDS (72 KB) and
@@ -263,7 +264,7 @@ __device__ __forceinline__ int wswz(int row, int chunk) {
   return row * 128 + ((chunk ^ (row & 7) ^ ((row >> 1) & 4)) << 4);
 }
 
-template <int W>
+template <int W, int kDist>  // kDist: steps between a staging chunk's global load and its LDS write
 __global__ void __launch_bounds__(256) conv3x3_halo_wgrad_kernel(const bf16_t* __restrict__ x,
                                                                 const bf16_t* __restrict__ dy,
                                                                 float* __restrict__ ws, int N, int H) {
@@ -281,34 +282,36 @@ __global__ void __launch_bounds__(256) conv3x3_halo_wgrad_kernel(const bf16_t* _
   const int b1 = (int)((long long)(blockIdx.x + 1) * total / gridDim.x);
 
   // a band's halo (hrows x 64 pixels, columns past W + 1 unused) and dy rows as 16-byte chunks, kXP + kDP per
-  // thread; branch-free: every lane loads from a clamped in-bounds address and out-of-range chunks are zeroed at
-  // the LDS write (a load under a lane condition splits the code into blocks, and the compiler then drains every
-  // outstanding load at the join instead of counting them).  LDS-DMA is not used: the compiler drains in-flight
-  // DMA before the first LDS read of each step, which serialised the next band's loads with this band's MFMAs.
+  // thread (global, not flat, loads: address_space(1)); halo pixels outside the image read the zero page, so no
+  // chunk needs a select after its load (the
+  // compiler hoists such selects right behind the loads and waits for them there).  Branch-free: a load under a
+  // lane condition splits the code into blocks, and the compiler then drains every outstanding load at the join.
+  // LDS-DMA is not used: the compiler drains in-flight DMA before the first LDS read of each step, which
+  // serialised the next band's loads with this band's MFMAs.
   constexpr int kXP = hrows * HP * 8 / 256, kDP = (dyrows * 8 + 255) / 256, kCH = kXP + kDP;
-  auto cload = [&](int band, int ci, bool& ok) {
+  auto cload = [&](int band, int ci) {
     const int n = band / bands, oh0 = (band - n * bands) * kTH;
-    long long off;
     if (ci < kXP) {
       const int i = tid + ci * 256, r = i >> 3, ch = i & 7;
       const int ih = oh0 - 1 + (r >> 6), iw = (r & 63) - 1;
-      ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      off = (((long long)n * H + (ok ? ih : oh0)) * W + (ok ? iw : 0)) * kC + ch * 8;
-    } else {
-      const int i = tid + (ci - kXP) * 256, r = i >> 3;
-      ok = r < npx;
-      off = (((long long)n * H + oh0) * W + (ok ? r : 0)) * kC + (i & 7) * 8;
+      const bool ok = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const long long off = (((long long)n * H + (ok ? ih : oh0)) * W + (ok ? iw : 0)) * kC + ch * 8;
+      return *reinterpret_cast<const __attribute__((address_space(1))) u32x4v*>((uintptr_t)sel(ok, x + off));
     }
-    return *reinterpret_cast<const u32x4v*>((ci < kXP ? x : dy) + off);
+    const int i = tid + (ci - kXP) * 256, r = i >> 3;
+    const bool ok = r < npx;
+    const long long off = (((long long)n * H + oh0) * W + (ok ? r : 0)) * kC + (i & 7) * 8;
+    return *reinterpret_cast<const __attribute__((address_space(1))) u32x4v*>((uintptr_t)sel(ok, dy + off));
   };
-  auto cstore = [&](lds_char* b, int ci, const u32x4v& v, bool ok) {
-    const u32x4v z = {0u, 0u, 0u, 0u}, w = ok ? v : z;
+  auto cstore = [&](lds_char* b, int ci, const u32x4v& w) {
     if (ci < kXP) {
       const int i = tid + ci * 256;
       *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(b + wswz(i >> 3, i & 7)) = w;
     } else {
       const int i = tid + (ci - kXP) * 256;
-      if (i < dyrows * 8)
+      // (unconditional when the chunks tile exactly: a conditional store makes the compiler sink its load into the
+      // branch, right before the store, where nothing hides its latency)
+      if (dyrows * 8 % 256 == 0 || i < dyrows * 8)
         *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(b + hbytes + wswz(i >> 3, i & 7)) = w;
     }
   };
@@ -342,65 +345,65 @@ __global__ void __launch_bounds__(256) conv3x3_halo_wgrad_kernel(const bf16_t* _
 
   if (b0 < b1) {
 #pragma unroll
-    for (int ci = 0; ci < kCH; ++ci) {
-      bool ok;
-      const u32x4v v = cload(b0, ci, ok);
-      cstore(smem, ci, v, ok);
-    }
+    for (int ci = 0; ci < kCH; ++ci) cstore(smem, ci, cload(b0, ci));
   }
   __syncthreads();
-  // next band's chunks: kPS per step, loaded at step st and written to the other buffer two steps later
+  // next band's chunks: kPS per step, loaded at step st and written to the other buffer kDist steps later (the
+  // last sets after the band's last step)
   constexpr int kPS = (kCH + nst - 2) / (nst - 1), kSets = (kCH + kPS - 1) / kPS;
   static_assert(kSets <= nst, "every chunk set is loaded within the band's steps");
   u32x4v stg[kSets][kPS];
-  bool sok[kSets][kPS];
   int cur = 0;
   for (int band = b0; band < b1; ++band) {
     const int nb = band + 1 < b1 ? band + 1 : band;  // the last band reloads itself into the unused buffer (no branch)
     lds_char* other = smem + (cur ^ 1) * bufb;  // its last readers passed the previous barrier
     const uint32_t buf = (uint32_t)(uintptr_t)(smem + cur * bufb);
-    v8bf a[4], b[9];
+    // fragments double-buffered: step st + 1's 26 reads are issued before step st's 36 MFMAs
+    v8bf a[2][4], b[2][9];
+    auto ldf = [&](int st, v8bf (&af)[4], v8bf (&bf)[9]) {
+      const int pix = 32 * st + 8 * g, orow = pix / W, w0 = pix - orow * W;
+      uint32_t rb = buf + (uint32_t)(orow * HP + w0) * 128u, fl = (uint32_t)((w0 >> 3) & 1) << 6;
+      asm volatile("" : "+v"(rb), "+v"(fl));  // this step's addresses are computed in this step (not hoisted)
+      const uint32_t ab = buf + st * 4096;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[0][i]));
+        const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[1][i]));
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[0][j] ^ fl) + rb));
+        const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[1][j] ^ fl) + rb));
+        bf[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    ldf(0, a[0], b[0]);
 #pragma unroll
     for (int st = 0; st < nst; ++st) {
       if (st < kSets) {
 #pragma unroll
         for (int k = 0; k < kPS; ++k)
-          if (st * kPS + k < kCH) stg[st][k] = cload(nb, st * kPS + k, sok[st][k]);
+          if (st * kPS + k < kCH) stg[st][k] = cload(nb, st * kPS + k);
       }
-      {
-        const int pix = 32 * st + 8 * g, orow = pix / W, w0 = pix - orow * W;
-        uint32_t rb = buf + (uint32_t)(orow * HP + w0) * 128u, fl = (uint32_t)((w0 >> 3) & 1) << 6;
-        asm volatile("" : "+v"(rb), "+v"(fl));  // this step's addresses are computed in this step (not hoisted)
-        const uint32_t ab = buf + st * 4096;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[0][i]));
-          const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)(ab + offA[1][i]));
-          a[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[0][j] ^ fl) + rb));
-          const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)((offB[1][j] ^ fl) + rb));
-          b[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-      }
+      if (st + 1 < nst) ldf(st + 1, a[(st + 1) & 1], b[(st + 1) & 1]);
 #pragma unroll
       for (int j = 0; j < 9; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      if (st >= 2 && st - 2 < kSets) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st & 1][i], b[st & 1][j], acc[i][j], 0, 0, 0);
+      if (st >= kDist && st - kDist < kSets) {
 #pragma unroll
         for (int k = 0; k < kPS; ++k)
-          if ((st - 2) * kPS + k < kCH) cstore(other, (st - 2) * kPS + k, stg[st - 2][k], sok[st - 2][k]);
+          if ((st - kDist) * kPS + k < kCH)
+            cstore(other, (st - kDist) * kPS + k, stg[st - kDist][k]);
       }
     }
 #pragma unroll
-    for (int s2 = nst - 2; s2 < kSets; ++s2)
+    for (int s2 = nst - kDist; s2 < kSets; ++s2)
 #pragma unroll
       for (int k = 0; k < kPS; ++k)
-        if (s2 * kPS + k < kCH) cstore(other, s2 * kPS + k, stg[s2][k], sok[s2][k]);
+        if (s2 * kPS + k < kCH) cstore(other, s2 * kPS + k, stg[s2][k]);
     __syncthreads();  // next band visible; every wave is done reading this one before it is overwritten
     cur ^= 1;
   }
@@ -472,7 +475,7 @@ static size_t halo_wgrad_lds() {
   return 2 * (size_t)(halo + dyb);
 }
 static int g_halo_wgrad = 1;
-void conv3x3_halo_wgrad_set(int on) { g_halo_wgrad = on; }
+void conv3x3_halo_wgrad_set(int on) { g_halo_wgrad = on; }  // 0 off, 1 on (2 / 3: shorter staging distance)
 
 int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
   if (!g_halo_wgrad || C != kC || K != kC || R != 3 || S != 3 || stride != 1 || pad != 1 ||
@@ -480,7 +483,11 @@ int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, in
     return 0;
   static int n_cu = 0;
   if (!n_cu) {
-    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_wgrad_kernel<kWgW>,
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_wgrad_kernel<kWgW, 2>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_wgrad_kernel<kWgW, 3>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_halo_wgrad_kernel<kWgW, 4>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     n_cu = halo_cus();
   }
@@ -489,7 +496,14 @@ int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, in
 }
 
 void conv3x3_halo_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int grid, int N, int H, hipStream_t st) {
-  hipLaunchKernelGGL(conv3x3_halo_wgrad_kernel<kWgW>, dim3(grid), dim3(256), halo_wgrad_lds(), st, x, dy, ws, N, H);
+  // staging distance: 4 steps (default; 2 / 3 by conv3x3_halo_wgrad_set(2 / 3) for A/B runs): 4 measured
+  // 312-319 us vs 331-335 us at 2 (profiles/r05_halo/wgrad3_dist_zp.log)
+  if (g_halo_wgrad == 2)
+    hipLaunchKernelGGL((conv3x3_halo_wgrad_kernel<kWgW, 2>), dim3(grid), dim3(256), halo_wgrad_lds(), st, x, dy, ws, N, H);
+  else if (g_halo_wgrad == 3)
+    hipLaunchKernelGGL((conv3x3_halo_wgrad_kernel<kWgW, 3>), dim3(grid), dim3(256), halo_wgrad_lds(), st, x, dy, ws, N, H);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_wgrad_kernel<kWgW, 4>), dim3(grid), dim3(256), halo_wgrad_lds(), st, x, dy, ws, N, H);
   DTG_LAUNCH_CHECK();
 }
 

@@ -23,8 +23,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--targets", default="256,512")
     ap.add_argument("--stages", default="1,2,3,4", help="which of the four stages to time")
+    ap.add_argument("--halo", type=int, default=1, help="conv_halo_wgrad_set value (stage 1: 0 implicit GEMM)")
     a = ap.parse_args()
     L, dev = lib(), torch.device("cuda")
+    L.conv_halo_wgrad_set(a.halo)
     shapes = [(64, 56), (128, 28), (256, 14), (512, 7)]
     for c, h in [shapes[int(i) - 1] for i in a.stages.split(",")]:
         x = torch.randn(a.n, h, h, c, device=dev).bfloat16()

@@ -7,3 +7,4 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 $R/tools/wgrad3_bench.py --stages 1 --targets 256 --iters 10 > $OUT/kt.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/p1 -o run -- python3 $R/tools/wgrad3_bench.py --stages 1 --targets 256 --iters 3 > $OUT/p1.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d $OUT/p2 -o run -- python3 $R/tools/wgrad3_bench.py --stages 1 --targets 256 --iters 3 > $OUT/p2.log 2>&1 || exit $?
