@@ -121,11 +121,13 @@ def test_hogwild_two_workers(tmp_path):
     out = run_cluster("Hogwild/Hogwild.py", 1, 2, ["--steps", "300", "--logdir", str(tmp_path / "l")])
     _ok(out)
     import re
-    vals = [float(re.search(r"\[\s*([-\d.e+]+)", l).group(1)) for l in out[("worker", 0)][1].splitlines()
+    # both elements of every printed c (the two start from different random values, so each is checked against its
+    # own trajectory)
+    vals = [[float(v) for v in re.findall(r"[-\d.e+]+", l)] for l in out[("worker", 0)][1].splitlines()
             if l.startswith("[")]
-    assert len(vals) == 30
-    gaps = [100 - v for v in vals]
-    assert all(b <= a + 1e-3 for a, b in zip(gaps, gaps[1:]))  # monotone toward 100
+    assert len(vals) == 30 and all(len(v) == 2 for v in vals)
+    gaps = [[100 - v for v in row] for row in vals]
+    assert all(b[e] <= a[e] + 1e-3 for a, b in zip(gaps, gaps[1:]) for e in range(2))  # monotone toward 100
     import dtg
     ck = dtg.train.latest_checkpoint(str(tmp_path / "l"))
     # the reference minimises without a global step (Hogwild/Hogwild.py:44), so its Supervisor writes a plain
@@ -136,7 +138,7 @@ def test_hogwild_two_workers(tmp_path):
     # the chief's final save holds its own 300 applies and whatever of the other worker's had landed: c moved
     # from ~0 most of the way a 300-step run gets toward 100
     c = r.get_tensor("Variable") + r.get_tensor("Variable_1")
-    assert all(100 - v <= gaps[-1] + 1e-3 for v in c)
+    assert all(100 - c[e] <= gaps[-1][e] + 1e-3 for e in range(2))
 
 
 def test_distributed_setup_mts():
