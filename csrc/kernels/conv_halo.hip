@@ -20,6 +20,10 @@ constexpr int kTH = 4, kC = 64;
 
 
 __device__ __forceinline__ int swz_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// LDS row of output channel k in the weight image: column n of n-tile j computes channel 4n + j, so a lane's four
+// accumulators of one pixel (j = 0..3) are 4 adjacent channels -- one 8-byte staging store instead of four 2-byte
+// ones -- while the B-fragment reads keep rows j*16 + n (conflict-free)
+__device__ __forceinline__ int wrow(int k) { return (k & 3) * 16 + (k >> 2); }
 
 // Persistent, software-pipelined form: one workgroup per CU keeps all 9 weight taps resident in LDS (72 KB) and
 // walks a contiguous run of bands with the halo double-buffered (2 x 44.5 KB at W = 56): the next band's halo
@@ -61,7 +65,7 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t = r*3 + s][k][c]
       const int ch = i & 7, k = (i >> 3) & 63, t = i >> 9;
       const u32x4v v = *reinterpret_cast<const u32x4v*>(w + ((long long)k * 9 + t) * kC + ch * 8);
-      *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(wt + t * 64 * 128 + swz_off(k, ch)) = v;
+      *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(wt + t * 64 * 128 + swz_off(wrow(k), ch)) = v;
     }
   } else {
     for (int i = tid; i < 9 * 64 * 8; i += 256) {  // w [k][r][s][c] -> wt[t][c][k] = w[k][8 - t][c]: 8 c per load
@@ -72,7 +76,7 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
       for (int e = 0; e < 8; ++e) {
         const int c = cc * 8 + e;
         const uint16_t h16 = (uint16_t)(e & 1 ? wd[e >> 1] >> 16 : wd[e >> 1] & 0xffffu);
-        *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wt + t * 64 * 128 + swz_off(c, k >> 3) +
+        *reinterpret_cast<__attribute__((address_space(3))) uint16_t*>(wt + t * 64 * 128 + swz_off(wrow(c), k >> 3) +
                                                                        (k & 7) * 2) = h16;
       }
     }
@@ -113,7 +117,7 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     const int oh = p / W, ow = p - oh * W;
     hbase[i] = oh * HW2 + ow;
   }
-  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};  // channel j*16 + lane%16
+  float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};  // channel 4 (lane % 16) + j
   float bs[8], bq[8];  // EPI 1: sum(dp), sum(dp * x) of channels 8 (lane & 7) + e over this lane's pixels
 #pragma unroll
   for (int e = 0; e < 8; ++e) bs[e] = bq[e] = 0.f;
@@ -161,21 +165,26 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     }
     __syncthreads();  // every wave is done with hbuf[cur]: reuse it for the output staging
     lds_char* st = hbuf[cur] + wave * 64 * 128;
+    typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int r = 0; r < 4; ++r) {
+        const int pr = i * 16 + g * 4 + r;
+        uint32_t hv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int pr = i * 16 + g * 4 + r, col = j * 16 + (lane & 15);
+        for (int j = 0; j < 4; ++j) {  // channel 4 (lane & 15) + j
           const bf16_t v = f2bf(acc[i][j][r]);
-          *reinterpret_cast<__attribute__((address_space(3))) bf16_t*>(st + pr * 128 + col * 2) = v;
+          hv[j] = (uint32_t)v;
           if constexpr (STATS) {  // rows past the band (duplicates) weigh 0
             const float f = wave * 64 + pr < npx ? bf2f(v) : 0.f;
             ssum[j] += f;
             ssq[j] += f * f;
           }
         }
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2v*>(st + pr * 128 + (lane & 15) * 8) =
+            u32x2v{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16)};
+      }
     __syncthreads();
     const long long out0 = px0;
 #pragma unroll
@@ -220,8 +229,8 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
       float* slot = part + (long long)(blockIdx.x % kBnStatSlots) * 2 * kC;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        atomicAdd(slot + j * 16 + lane, ssum[j]);
-        atomicAdd(slot + kC + j * 16 + lane, ssq[j]);
+        atomicAdd(slot + 4 * lane + j, ssum[j]);
+        atomicAdd(slot + kC + 4 * lane + j, ssq[j]);
       }
     }
   }
