@@ -65,6 +65,13 @@ def parse(argv=None):
     ap.add_argument("--mode", default="sync", choices=("sync", "async_ps"))
     ap.add_argument("--window", type=int, default=1, help="async_ps: local steps per push (DOWNPOUR/ADAG window)")
     ap.add_argument("--overlap_pull", type=int, default=1, help="async_ps: pull overlapped with the next step")
+    ap.add_argument("--window_mode", default="sum", choices=("sum", "mean"),
+                    help="async_ps: push the window's sum (DOWNPOUR) or mean (ADAG)")
+    ap.add_argument("--local_opt", default="none", choices=("none", "sgd", "adagrad", "momentum"),
+                    help="async_ps: worker-local optimizer inside the window (DOWNPOUR: adagrad, ADAG: sgd)")
+    ap.add_argument("--local_lr", type=float, default=None, help="async_ps: local optimizer lr (default: --lr)")
+    ap.add_argument("--ps_opt", default="momentum", choices=("sgd", "adagrad", "momentum"),
+                    help="async_ps: the PS's global optimizer (DOWNPOUR: adagrad, ADAG: sgd)")
     return ap.parse_known_args(argv)[0]
 
 
@@ -198,13 +205,14 @@ def main(argv=None):
         step = GraphedStep(step, warmup=min(2, max(a.warmup - 1, 1)))
     main_prio = os.environ.get("DTG_MAIN_PRIO")
     if (main_prio is None and a.model == "bert" and world == 1 and os.environ.get("DTG_DDP_FORCE") != "1"
-            and "DTG_SIDE_PRIO" not in os.environ):
+            and "DTG_SIDE_PRIO" not in os.environ and not use_graph):
         # BERT on one rank (no collective stream): the main stream (data gradients, LayerNorm, attention -- the
         # critical path) on the high-priority queue and the weight-gradient side stream at normal priority, so
         # the side stream's compute-bound GEMMs fill in around the main stream instead of taking CUs from it:
         # 9,466 vs 9,345 seq/s (profiles/r05_stream_prio/ab_bert_prio.log).  ResNet-50 measured the opposite
         # (its side stream must keep pace with a memory-bound main stream), and with ranks > 1 the process
-        # group's high-priority stream needs its own queue, so both keep the default order.
+        # group's high-priority stream needs its own queue, so both keep the default order.  Not under a graph
+        # replay (--graph 1): the main stream is not re-created there, so only the side stream would move.
         from dtg.parallel import overlap as _ov
         _ov.set_side_priority(0)
         main_prio = "-1"
@@ -322,7 +330,9 @@ def _allreduce_probe(dp, bucket_mb, world, device, sync):
 
 def _async_ps(a, rank, world, device):
     """BASELINE.json config 4: 1 PS + (N-1) ResNet-50 workers, Hogwild by default
-    (``--window T``: DOWNPOUR-style sum of T local gradients per push).  The PS rank owns a GPU and the
+    (``--window T``: sum (DOWNPOUR) or ``--window_mode mean`` (ADAG) of T local gradients per push, with
+    ``--local_opt adagrad|sgd`` taking T - 1 worker-local optimizer steps inside the window and ``--ps_opt`` the
+    PS's global rule -- DOWNPOUR = ``--local_opt adagrad --ps_opt adagrad``).  The PS rank owns a GPU and the
     parameters; workers push gradients and pull parameters over RCCL point-to-point (parallel/async_ps.py).
     Whole-node images/sec = PS-applied updates x images per update / wall time, counted on the PS from the
     moment every worker has finished its W warm-up steps (a device synchronize on the PS brackets both
@@ -331,7 +341,7 @@ def _async_ps(a, rank, world, device):
     import torch
     from dtg import ops
     from dtg.models import resnet
-    from dtg.optim import FusedSGD
+    from dtg.optim import make_optimizer
     from dtg.parallel import FlatParams, comm
     from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
     if world < 2:
@@ -345,9 +355,11 @@ def _async_ps(a, rank, world, device):
     model = resnet.resnet50().to(device).to(memory_format=torch.channels_last)
     flat = FlatParams(model)
     dtype = torch.bfloat16 if device.type == "cuda" else torch.float32
+    lr = a.lr or 0.1
     if rank == 0:
-        opt = FusedSGD(flat, lr=a.lr or 0.1, momentum=0.9, weight_decay=5e-5)
-        ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, staleness_log=True)
+        opt = make_optimizer(a.ps_opt, flat, lr, momentum=0.9, weight_decay=5e-5)
+        ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, window_mode=a.window_mode,
+                           staleness_log=True)
         ps.serve()
         (u0, t0), (u1, t1) = ps.timed or ps.timed_end, ps.timed_end
         imgs = (u1 - u0) * a.batch * a.window
@@ -362,12 +374,15 @@ def _async_ps(a, rank, world, device):
             "config": {"model": "ResNet-50", "per_gpu_batch": a.batch, "global_batch": a.batch * (world - 1),
                        "image_size": a.image, "parallelism": "ps1+w%d" % (world - 1),
                        "transport": "rccl p2p" if _backend_name() == "rccl" else _backend_name(),
-                       "window": a.window, "overlap_pull": bool(a.overlap_pull), "optimizer": "momentum-sgd (fused, on PS)"},
+                       "window": a.window, "window_mode": a.window_mode, "local_opt": a.local_opt,
+                       "overlap_pull": bool(a.overlap_pull), "optimizer": "%s (fused, on PS)" % a.ps_opt},
             "updates_timed": u1 - u0, "per_worker": {str(k): v for k, v in ps.per_worker.items()},
             "mean_staleness": round(sum(st) / len(st), 3), "lost_workers": ps.lost}), flush=True)
         ps.close()
     else:
-        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, overlap_pull=bool(a.overlap_pull))
+        local = make_optimizer(a.local_opt, flat, a.local_lr or lr) if a.window > 1 else None
+        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode, local_optimizer=local,
+                          overlap_pull=bool(a.overlap_pull))
         x, y = resnet.synthetic_batch(a.batch, device, dtype, a.image, 1000, seed=rank)
         model.train()
         w.begin()

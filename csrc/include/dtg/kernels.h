@@ -255,7 +255,8 @@ int conv_supported(int C, int K, int R, int S, int stride, int pad, int which);
 // direct 3x3 / s1 / p1 conv, 64 -> 64 channels, with the BN forward statistics into part (conv_halo.hip; conv_fwd
 // takes it for BnEpi mode 1 when conv3x3_halo_bn_ok)
 int conv3x3_halo_bn_ok(int C, int K, int H, int W);
-void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st);
+bool conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st);
+void conv3x3_halo_fwd_set(int on);  // (A/B tools, tests) the halo forward on / off
 // its data gradient with the BN-backward mode-3 epilogue (packed mask bits, beta 0); false if bn is not that form
 bool conv3x3_halo_bn_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dp, int N, int H, int W, const BnEpi& bn,
                            hipStream_t st);

@@ -486,10 +486,8 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
               int stride, int pad, hipStream_t st, const BnEpi& bn) {
   // 64 -> 64 3x3 / s1 / p1 with the BN statistics (ResNet-50 stage 1): the direct halo-tile conv (conv_halo.hip)
   if (bn.mode == 1 && R == 3 && S == 3 && stride == 1 && pad == 1 && g_conv_tile[0] == 0 && g_conv_stages[0] <= 0 &&
-      conv3x3_halo_bn_ok(C, K, H, W)) {
-    conv3x3_halo_bn_fwd(x, w, y, N, H, W, bn.part, st);
+      conv3x3_halo_bn_ok(C, K, H, W) && conv3x3_halo_bn_fwd(x, w, y, N, H, W, bn.part, st))
     return;
-  }
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   const int M = N * G.P * G.Q;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};

@@ -118,9 +118,20 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
     hbase[i] = oh * HW2 + ow;
   }
   float ssum[4] = {0.f, 0.f, 0.f, 0.f}, ssq[4] = {0.f, 0.f, 0.f, 0.f};  // channel 4 (lane % 16) + j
-  float bs[8], bq[8];  // EPI 1: sum(dp), sum(dp * x) of channels 8 (lane & 7) + e over this lane's pixels
+  // EPI 1: sum(dp), sum(dp * xhat) of channels 8 (lane & 7) + e over this lane's pixels; xhat is formed per element
+  // (x * invstd - mean * invstd) from the lane's 8 fixed channels, like the implicit-GEMM epilogue -- a raw-moment
+  // form, invstd * (sum(dp * x) - mean * sum(dp)), cancels when |mean| >> std
+  float bs[8], bq[8], xs[8], xo[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs[e] = bq[e] = 0.f;
+  for (int e = 0; e < 8; ++e) {
+    bs[e] = bq[e] = 0.f;
+    xs[e] = xo[e] = 0.f;
+    if constexpr (EPI == 1) {
+      const int c = (lane & 7) * 8 + e;
+      xs[e] = hb.invstd[c];
+      xo[e] = -hb.mean[c] * xs[e];
+    }
+  }
   int cur = 0;
   for (int band = b0; band < b1; ++band) {
     if (band + 1 < b1) gload(band + 1);
@@ -204,8 +215,10 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
             const float dl = __uint_as_float(lo << 16), dh = __uint_as_float(hi);
             bs[2 * e2] += dl;
             bs[2 * e2 + 1] += dh;
-            bq[2 * e2] = fmaf(dl, __uint_as_float(xd[e2] << 16), bq[2 * e2]);
-            bq[2 * e2 + 1] = fmaf(dh, __uint_as_float(xd[e2] & 0xffff0000u), bq[2 * e2 + 1]);
+            const float xl = fmaf(__uint_as_float(xd[e2] << 16), xs[2 * e2], xo[2 * e2]);
+            const float xh = fmaf(__uint_as_float(xd[e2] & 0xffff0000u), xs[2 * e2 + 1], xo[2 * e2 + 1]);
+            bq[2 * e2] = fmaf(dl, xl, bq[2 * e2]);
+            bq[2 * e2 + 1] = fmaf(dh, xh, bq[2 * e2 + 1]);
           }
           v.x = od[0]; v.y = od[1]; v.z = od[2]; v.w = od[3];
         }
@@ -248,7 +261,7 @@ __global__ void __launch_bounds__(256) conv3x3_halo_pp_kernel(const bf16_t* __re
       for (int e = 0; e < 8; ++e) {
         const int c = lane * 8 + e;
         atomicAdd(slot + c, bs[e]);
-        atomicAdd(slot + kC + c, hb.invstd[c] * (bq[e] - hb.mean[c] * bs[e]));  // sum(dp * xhat)
+        atomicAdd(slot + kC + c, bq[e]);  // sum(dp * xhat)
       }
     }
   }
@@ -452,12 +465,17 @@ static int halo_cus() {
   return n_cu;
 }
 
-void conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st) {
+static int g_halo_fwd = 1;
+void conv3x3_halo_fwd_set(int on) { g_halo_fwd = on; }  // 0 off (implicit GEMM), 1 on
+
+bool conv3x3_halo_bn_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, float* part, hipStream_t st) {
+  if (!g_halo_fwd) return false;
   const int n_cu = halo_cus(), total = N * (H / kTH);
   const dim3 grid(total < n_cu ? total : n_cu);
   hipLaunchKernelGGL(conv3x3_halo_pp_kernel<0>, grid, dim3(256), halo_bn_lds(W), st, x, w, y, N, H, W, part,
                      HaloBwd{});
   DTG_LAUNCH_CHECK();
+  return true;
 }
 
 static int g_halo_dgrad = 1;

@@ -1,8 +1,8 @@
 // PyTorch bindings of the GEMM / conv lab kernels (module dtg._lab, built only by tools/build_ext.py --only lab and
 // imported through dtg.ops._native.lab()): A/B candidates and negative results that are not part of the production
-// extension _C -- the 256x256 8-phase GEMMs (gemm8.hip), the forced tile table (gemm_forced*.hip), the direct 3x3
-// halo conv (conv_halo.hip), the round-5 main-loop lab (gemm5.hip) and the transposed fused BN dx +
-// weight gradient (bn_dxT_wgrad.hip).
+// extension _C -- the 256x256 8-phase GEMMs (gemm8.hip), the forced tile table (gemm_forced*.hip), the round-5
+// main-loop lab (gemm5.hip) and the transposed fused BN dx + weight gradient (bn_dxT_wgrad.hip).  (The round-3 halo
+// conv fork was retired in round 6: the production csrc/kernels/conv_halo.hip is the one tested and benchmarked.)
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -133,27 +133,6 @@ bool gemm_cfg(int64_t cfg, Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor out,
                            (int)act, sk, wsp, cur_stream(), auxp, (int)aux_mode);
 }
 
-void check_nhwc64(const Tensor& x, const Tensor& w) {
-  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.is_contiguous() && w.is_contiguous(), "contiguous GPU tensors");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16");
-  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 3 &&
-                  w.size(3) == x.size(3), "x [N, H, W, C], w [64, 3, 3, C]");
-}
-
-// direct 3x3 conv (C = K = 64, stride 1, pad 1) from an LDS halo tile; with_stats: + BN statistics partials
-std::tuple<Tensor, Tensor> conv_halo_fwd(Tensor x, Tensor w, bool with_stats) {
-  check_nhwc64(x, w);
-  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  TORCH_CHECK(dtg::conv3x3_halo_supported(C, 64, H, W, with_stats ? 1 : 0), "conv_halo_fwd: unsupported shape");
-  c10::DeviceGuard dg(x.device());
-  auto y = at::empty({N, H, W, 64}, x.options());
-  Tensor part;
-  if (with_stats) part = at::zeros({(long long)dtg::kBnStatSlots * 2 * 64}, x.options().dtype(at::kFloat));
-  dtg::conv3x3_halo_fwd(cbfp(x), cbfp(w), bfp(y), N, H, W, cur_stream(),
-                        with_stats ? part.data_ptr<float>() : nullptr);
-  return {y, part};
-}
-
 }  // namespace
 
 PYBIND11_MODULE(_lab, m) {
@@ -168,5 +147,4 @@ PYBIND11_MODULE(_lab, m) {
         pybind11::arg("aux") = pybind11::none(), pybind11::arg("aux_mode") = 0);
   m.def("bn_dxT_wgrad", &bn_dxT_wgrad, pybind11::arg("dp"), pybind11::arg("x"), pybind11::arg("coef"),
         pybind11::arg("act"), pybind11::arg("wgrad"));
-  m.def("conv_halo_fwd", &conv_halo_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("with_stats") = false);
 }

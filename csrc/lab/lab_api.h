@@ -8,10 +8,5 @@ namespace dtg {
 bool gemm_lab_cfg(int cfg, const bf16_t* A, long long lda, int a_kc, const bf16_t* B, long long ldb, int b_kc, void* C,
                   long long ldc, int c_bf16, int M, int N, int K, float alpha, float beta, const float* bias, int act,
                   int split_k, float* ws, hipStream_t st, void* aux, int aux_mode);
-// Direct 3x3 / stride 1 / pad 1 conv for C = K = 64 from an LDS halo tile (conv_halo.hip); with part, also the
-// BatchNorm forward statistics (BnEpi mode 1 partials).  Neutral in the ResNet-50 step (profiles/r04_conv_halo).
-int conv3x3_halo_supported(int C, int K, int H, int W, int stats = 0);
-void conv3x3_halo_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, hipStream_t st,
-                      float* part = nullptr);
 
 }  // namespace dtg

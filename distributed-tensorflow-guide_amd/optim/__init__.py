@@ -1,2 +1,2 @@
 """Optimizers: fused flat-buffer applies (north-star models)."""
-from .fused import FusedSGD, FusedAdam, FusedAdagrad  # noqa: F401
+from .fused import FusedSGD, FusedAdam, FusedAdagrad, make_optimizer  # noqa: F401

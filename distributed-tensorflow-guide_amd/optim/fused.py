@@ -114,9 +114,32 @@ class FusedAdagrad(_FlatOptimizer):
         self.init_acc = initial_accumulator_value
         self.eps = eps
 
+    def _acc(self, g):
+        # the WHOLE group's accumulator is created and filled with the initial value on first use: DataParallel.step
+        # applies a group slice by slice (_Slice shares the group's state dict), so a per-slice "fresh" test would
+        # fill only the first slice and leave later slices at the allocator's zeros (lr * sign(g), or 0/0)
+        full = g._g if isinstance(g, _Slice) else g
+        if "acc" not in full.state:
+            full.state_buffer("acc").fill_(self.init_acc)
+        return g.state_buffer("acc")
+
     def _apply(self, g, gscale, zero_grad):
-        fresh = "acc" not in g.state
-        acc = g.state_buffer("acc")
-        if fresh:
-            acc.fill_(self.init_acc)
-        K.adagrad(g.master, g.grad, acc, self.hyper, g.mirror, self.eps, gscale, zero_grad)
+        K.adagrad(g.master, g.grad, self._acc(g), self.hyper, g.mirror, self.eps, gscale, zero_grad)
+
+
+def make_optimizer(kind, flat, lr, **kw):
+    """A fused flat optimizer by name, for the CLI flags of the async-PS examples and bench (``--local_opt``,
+    ``--ps_opt``): ``sgd`` plain SGD (TF GradientDescentOptimizer, ADAG's local and global rule), ``momentum``
+    momentum 0.9 SGD, ``adagrad`` TF Adagrad with initial accumulator 0.1 (DOWNPOUR's local and global rule,
+    /root/reference/DOWNPOUR/DOWNPOUR.py:57, :92), ``adam`` AdamW.  ``none`` returns None."""
+    if kind in (None, "none"):
+        return None
+    if kind == "sgd":
+        return FusedSGD(flat, lr=lr, momentum=0.0)
+    if kind == "momentum":
+        return FusedSGD(flat, lr=lr, momentum=kw.get("momentum", 0.9), weight_decay=kw.get("weight_decay", 0.0))
+    if kind == "adagrad":
+        return FusedAdagrad(flat, lr=lr)
+    if kind == "adam":
+        return FusedAdam(flat, lr=lr, weight_decay=kw.get("weight_decay", 0.01))
+    raise ValueError("unknown optimizer %r (sgd, momentum, adagrad, adam, none)" % (kind,))

@@ -302,10 +302,16 @@ class AsyncPSWorker:
         True when an exchange with the PS happened."""
         self.local_step += 1
         if self._acc is not None:
-            # DOWNPOUR-style: accumulate this step's gradient, then take a local optimizer step
+            # DOWNPOUR-style: accumulate this step's gradient, then take a local optimizer step -- on the first T - 1
+            # steps of the window only, as the reference's graph runs it (DOWNPOUR/DOWNPOUR.py:65-75: the t-th
+            # compute_gradients waits for opt_local of step t - 1, and nothing waits for the last one, so a window
+            # of T gradient evaluations applies T - 1 local updates; SURVEY App. B #5).  The last local update
+            # would be overwritten by the pull anyway, but it would still feed the local optimizer's state (an
+            # Adagrad accumulator, a momentum buffer) a gradient the reference never applies locally.
             for a, g in zip(self._acc, self.flat):
                 a.add_(g.grad.to(a.dtype))
-            self.local_opt.step()
+            if self.local_step % self.window:
+                self.local_opt.step()
         if self.local_step % self.window:
             return False
         self._land_pull()
@@ -424,15 +430,28 @@ class AsyncPSServer:
         self.order.append((w, self._push_idx[w]))
         self._push_idx[w] += 1
 
-    def _bound_inflight(self):
-        """Record this request's completion on the apply stream; wait for the oldest beyond max_inflight."""
+    def _bound_inflight(self, w):
+        """Record this request's completion on the apply stream; wait for the oldest beyond max_inflight.
+
+        The wait polls the event against ``worker_timeout`` instead of blocking in ``synchronize()``: a worker that
+        died mid-transfer leaves its receive (and so the apply stream behind it) pending forever, and the host must
+        still fail-stop with a TimeoutError naming that worker, as the module docstring promises."""
         if self.dev.type != "cuda":
             return
+        import time
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.dev))
-        self._inflight.append(ev)
+        self._inflight.append((ev, w))
         while len(self._inflight) > self.max_inflight:
-            self._inflight.pop(0).synchronize()
+            ev0, w0 = self._inflight.pop(0)
+            deadline = time.monotonic() + self.worker_timeout
+            nap = 5e-5
+            while not ev0.query():
+                if time.monotonic() > deadline:
+                    raise TimeoutError("async PS: the request of worker rank %d has not completed on the device in "
+                                       "%.0f s (worker lost mid-transfer?)" % (w0, self.worker_timeout))
+                time.sleep(nap)
+                nap = min(nap * 2, 2e-3)
 
     def _grad(self, w):
         # the receive is posted from the apply (current) stream, so RCCL's pair stream first waits for the
@@ -442,7 +461,7 @@ class AsyncPSServer:
         _wait_all([_irecv(b, w, self.pg) for b in self._recv[w] + self._recv_buf[w]])
         self._apply(w)
         self._send_params(w)
-        self._bound_inflight()
+        self._bound_inflight(w)
 
     def _elastic(self, w):
         """EASGD exchange (Zhang, Choromanska, LeCun 2015): receive the worker's parameters x_i,

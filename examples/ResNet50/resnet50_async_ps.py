@@ -5,7 +5,14 @@ but the PS owns a GPU and the parameters live in its HBM (dtg.parallel.async_ps)
 
     bash run_async.sh [--workers 7] [--steps 50] [--window 1]
 
---window T > 1 pushes every T local steps: --window_mode sum = DOWNPOUR, mean = ADAG.
+--window T > 1 pushes every T local steps: --window_mode sum = DOWNPOUR, mean = ADAG.  --local_opt takes T - 1
+worker-local optimizer steps inside the window and --ps_opt picks the PS's global rule, as in the reference:
+
+    DOWNPOUR       --window 3 --window_mode sum  --local_opt adagrad --ps_opt adagrad   (DOWNPOUR/DOWNPOUR.py:57, :92)
+    DOWNPOUR-Easy  --window 3 --window_mode sum  --local_opt sgd     --ps_opt adagrad   (DOWNPOUR-Easy/DOWNPOUR.py:53)
+    ADAG           --window 3 --window_mode mean --local_opt sgd     --ps_opt sgd       (ADAG/ADAG.py:61-63)
+
+Without --local_opt a window sums T gradients taken at the same parameters (SDAG's degenerate window).
 """
 import argparse
 import time
@@ -17,7 +24,7 @@ import torch
 import dtg  # noqa: F401
 from dtg import ops
 from dtg.models import resnet
-from dtg.optim import FusedSGD
+from dtg.optim import make_optimizer
 from dtg.parallel import FlatParams
 from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker, init_from_cluster
 
@@ -34,6 +41,11 @@ def main():
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--window", type=int, default=1)
     ap.add_argument("--window_mode", default="sum", choices=("sum", "mean"))
+    ap.add_argument("--local_opt", default="none", choices=("none", "sgd", "adagrad", "momentum"),
+                    help="worker-local optimizer inside the window (T - 1 local steps)")
+    ap.add_argument("--local_lr", type=float, default=None, help="local optimizer learning rate (default --lr)")
+    ap.add_argument("--ps_opt", default="momentum", choices=("sgd", "adagrad", "momentum"),
+                    help="the PS's global optimizer")
     ap.add_argument("--dyn_sgd", action="store_true",
                     help="Dynamic SGD: scale each PS update by 1/(staleness+1) (reference README TODO)")
     ap.add_argument("--overlap_pull", action="store_true",
@@ -49,7 +61,7 @@ def main():
     ncls = 10 if a.tiny else 1000
     flat = FlatParams(model)
     if a.job_name == "ps":
-        opt = FusedSGD(flat, lr=a.lr, momentum=0.9, weight_decay=5e-5)
+        opt = make_optimizer(a.ps_opt, flat, a.lr, momentum=0.9, weight_decay=5e-5)
         ps = AsyncPSServer(flat, opt, workers=range(1, world), window=a.window, window_mode=a.window_mode,
                            staleness_log=True, staleness_scaling="dyn" if a.dyn_sgd else None)
         t0 = time.time()
@@ -59,7 +71,9 @@ def main():
         print(f"[ps] {n} updates in {dt:.1f}s, per worker {ps.per_worker}, mean staleness "
               f"{sum(st) / max(1, len(st)):.2f}", flush=True)
     else:
-        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode, overlap_pull=a.overlap_pull)
+        local = make_optimizer(a.local_opt, flat, a.local_lr or a.lr) if a.window > 1 else None
+        w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode, local_optimizer=local,
+                          overlap_pull=a.overlap_pull)
         dt_ = torch.bfloat16 if device.type == "cuda" else torch.float32
         x, y = resnet.synthetic_batch(a.batch, device, dt_, a.image, ncls, seed=rank)
         w.begin()

@@ -486,3 +486,173 @@ def test_announcer_sends_tokens_only_after_their_events_in_order():
     a.close()
     assert [k for _, k, _ in sent] == [1, 4, 2]
     assert sent[0][2] - t0 >= 0.3 and e1.done.is_set()
+
+
+# ---- DOWNPOUR / ADAG with a worker-local optimizer (/root/reference/DOWNPOUR/DOWNPOUR.py:54-102,
+# /root/reference/ADAG/ADAG.py:61-90): pull, T gradient evaluations with T - 1 local optimizer updates between them,
+# push the window's sum (DOWNPOUR) or mean (ADAG), global optimizer on the PS, pull.
+
+_LR_G, _LR_L = 0.05, 0.02
+
+
+def _make_opt(kind, flat, lr):
+    from dtg.optim import FusedAdagrad, FusedSGD
+    return FusedAdagrad(flat, lr=lr) if kind == "adagrad" else FusedSGD(flat, lr=lr, momentum=0.0)
+
+
+def _rank_local(rank, world, port, steps, window, mode, local, glob, q):
+    try:
+        sys.path.insert(0, ROOT)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        import dtg  # noqa: F401
+        from dtg import ops
+        from dtg.parallel import FlatParams, comm
+        from dtg.parallel.async_ps import AsyncPSServer, AsyncPSWorker
+        comm.init("gloo")
+        model = _model()
+        flat = FlatParams(model, compute_dtype=torch.float32)
+        if rank == 0:
+            ps = AsyncPSServer(flat, _make_opt(glob, flat, _LR_G), workers=range(1, world), window=window,
+                               window_mode=mode)
+            n = ps.serve()
+            q.put((rank, "ok", {"updates": n, "order": list(ps.order), "w": [g.master.clone().numpy() for g in flat]}))
+        else:
+            w = AsyncPSWorker(flat, ps_rank=0, window=window, window_mode=mode,
+                              local_optimizer=_make_opt(local, flat, _LR_L))
+            w.begin()
+            x, y = _data(rank)
+            for _ in range(steps):
+                ops.softmax_cross_entropy(model(x), y).backward()
+                w.step_done()
+            w.finish()
+            q.put((rank, "ok", {"pushes": w.pushes}))
+        comm.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc(), None))
+        raise
+
+
+def _run_local(world, steps, window, mode, local, glob):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    port = free_ports(1)[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_local, args=(r, world, port, steps, window, mode, local, glob, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, status, payload = q.get(timeout=240)
+        assert status == "ok", status
+        out[r] = payload
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+class _Rule:
+    """TF ApplyAdagrad (initial accumulator 0.1) or ApplyGradientDescent on a dict of named tensors."""
+
+    def __init__(self, kind, lr, like):
+        self.kind, self.lr = kind, lr
+        self.acc = {n: torch.full_like(v, 0.1) for n, v in like.items()} if kind == "adagrad" else None
+
+    def apply(self, params, grads):
+        for n in params:
+            g = grads[n]
+            if self.acc is not None:
+                self.acc[n].add_(g * g)
+                params[n] = params[n] - self.lr * g * torch.rsqrt(self.acc[n])
+            else:
+                params[n] = params[n] - self.lr * g
+
+
+def _window_replay(order, window, mode, local, glob):
+    """Sequential replay of the reference rule in the PS's applied order: worker w's window k starts from the PS
+    state its previous pull returned (the state right after ITS previous update; the initial state for k = 0)."""
+    import dtg  # noqa: F401
+    from dtg import ops
+    model = _model()
+    names = [n for n, _ in model.named_parameters()]
+    state = {n: p.detach().clone() for n, p in model.named_parameters()}
+    gopt = _Rule(glob, _LR_G, state)
+    pulled, lopt = {}, {}
+    for w, k in order:
+        start = pulled.get(w, {n: v.clone() for n, v in _model().named_parameters()})
+        lopt.setdefault(w, _Rule(local, _LR_L, state))
+        x, y = _data(w)
+        loc = {n: v.detach().clone() for n, v in start.items()}
+        total = {n: torch.zeros_like(v) for n, v in loc.items()}
+        for t in range(window):
+            with torch.no_grad():
+                for n, p in model.named_parameters():
+                    p.copy_(loc[n])
+            loss = ops.softmax_cross_entropy(model(x), y)
+            grads = dict(zip(names, torch.autograd.grad(loss, list(model.parameters()))))
+            for n in names:
+                total[n] += grads[n]
+            if t < window - 1:  # T - 1 local updates (DOWNPOUR/DOWNPOUR.py:65-75)
+                lopt[w].apply(loc, grads)
+        push = {n: v / window for n, v in total.items()} if mode == "mean" else total
+        gopt.apply(state, push)
+        pulled[w] = {n: v.clone() for n, v in state.items()}
+    return state
+
+
+@pytest.mark.parametrize("local,glob,mode", [("adagrad", "adagrad", "sum"),  # DOWNPOUR
+                                             ("sgd", "adagrad", "sum"),      # DOWNPOUR-Easy
+                                             ("sgd", "sgd", "mean")])        # ADAG
+def test_async_ps_local_optimizer_window_equals_reference_rule(local, glob, mode):
+    """1 PS + 1 worker, window 3 with a local optimizer: the PS parameters equal a sequential replay of the
+    reference's rule (T gradients, T - 1 local applies, summed / averaged push, global apply on the PS)."""
+    out = _run_local(2, steps=12, window=3, mode=mode, local=local, glob=glob)
+    assert out[0]["updates"] == 4 and out[1]["pushes"] == 4
+    ref = _window_replay(out[0]["order"], 3, mode, local, glob)
+    got = _ps_params_by_name(out)
+    for n, v in ref.items():
+        assert torch.allclose(got[n], v, atol=1e-5), (n, (got[n] - v).abs().max())
+
+
+def test_async_ps_downpour_two_workers_follow_logged_order():
+    """1 PS + 2 workers, DOWNPOUR (local Adagrad, window 3, global Adagrad): whatever order the PS applied the
+    pushes in, replaying that logged order with each worker's window starting from the state its own previous pull
+    returned gives the PS's final parameters."""
+    out = _run_local(3, steps=9, window=3, mode="sum", local="adagrad", glob="adagrad")
+    order = out[0]["order"]
+    assert out[0]["updates"] == 6 and sorted(order) == [(1, 0), (1, 1), (1, 2), (2, 0), (2, 1), (2, 2)]
+    ref = _window_replay(order, 3, "sum", "adagrad", "adagrad")
+    got = _ps_params_by_name(out)
+    for n, v in ref.items():
+        assert torch.allclose(got[n], v, atol=1e-5), (n, (got[n] - v).abs().max())
+
+
+def test_bound_inflight_times_out_naming_the_worker(monkeypatch):
+    """the PS host's wait for its oldest in-flight request polls against worker_timeout and raises a
+    TimeoutError naming the worker (a receive from a worker that died mid-transfer never completes), instead of
+    blocking forever in Event.synchronize()."""
+    import types
+    import dtg  # noqa: F401
+    from dtg.parallel import async_ps
+
+    class NeverDone:
+        def record(self, stream):
+            pass
+
+        def query(self):
+            return False
+
+        def synchronize(self):  # pragma: no cover - the old, unbounded wait
+            raise AssertionError("blocking synchronize() on an in-flight request")
+
+    monkeypatch.setattr(torch.cuda, "Event", NeverDone)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda dev=None: None)
+    ps = object.__new__(async_ps.AsyncPSServer)
+    ps.dev = types.SimpleNamespace(type="cuda")
+    ps.max_inflight, ps.worker_timeout, ps._inflight = 1, 0.3, []
+    ps._bound_inflight(3)
+    with pytest.raises(TimeoutError, match="worker rank 3"):
+        ps._bound_inflight(5)

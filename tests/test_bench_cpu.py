@@ -58,6 +58,21 @@ def test_async_ps_mode_reports_whole_node_rate():
     assert 1 <= j["updates_timed"] <= 8
 
 
+def test_async_ps_mode_downpour_window_with_local_optimizer():
+    """bench.py --mode async_ps in its DOWNPOUR form (--window 3, local Adagrad inside the window, Adagrad on the
+    PS; /root/reference/DOWNPOUR/DOWNPOUR.py:54-102): every worker pushes once per window and the JSON line names
+    the rule."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--mode", "async_ps",
+                        "--batch", "2", "--image", "32", "--steps", "3", "--warmup", "3", "--window", "3",
+                        "--local_opt", "adagrad", "--ps_opt", "adagrad", "--lr", "0.01"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    j = _json_line(r.stdout)
+    c = j["config"]
+    assert c["window"] == 3 and c["local_opt"] == "adagrad" and c["optimizer"].startswith("adagrad"), c
+    assert j["per_worker"] == {"1": 2} and j["lost_workers"] == []
+
+
 def test_driver_launch_form_eight_ranks_resnet():
     """The round-end scaling run's exact launch form (torch.distributed.run, 8 ranks on 127.0.0.1, bench.py
     --gpus 8) with the headline model, shrunk to 32x32 images and batch 2 per rank on gloo: one JSON line

@@ -149,25 +149,32 @@ def test_conv_bn_fwd_and_dgrad_stats(C, K, H, R, st, pad):
         assert _rel(s3, sr) < 1e-2 and _rel(q3, qr) < 1e-2
 
 
-@pytest.mark.parametrize("N,H", [(2, 56), (3, 28)])
-def test_conv_dgrad_bn_halo_64(N, H):
+@pytest.mark.parametrize("N,H,grid,shift", [(2, 56, 1, 0.0), (3, 28, 1, 0.0), (40, 56, 1, 0.0), (40, 56, 192, 0.0),
+                                             (5, 56, 1, 64.0)])
+def test_conv_dgrad_bn_halo_64(N, H, grid, shift):
     """conv_dgrad_bn with packed mask bits for ResNet's stage-1 3x3 (64 -> 64, s1, p1) runs the direct halo-tile
     data gradient (csrc/kernels/conv_halo.hip, EPI 1): against the fp32 reference and against the implicit-GEMM
-    dgrad (conv_halo_dgrad_set(0)) with the same epilogue."""
+    dgrad (conv_halo_dgrad_set(0)) with the same epilogue.  N = 40 at 56x56 is 560 bands: every one of the 256
+    persistent workgroups walks 2-3 bands through the double-buffered halo (the benchmark's b1024 walks ~56);
+    grid 192 (conv_halo_dgrad_set(192)) gives uneven runs of 2 and 3 bands; shift 64 puts the BN input's mean at
+    64x its standard deviation, where a raw-moment sum(dp * x) - mean * sum(dp) would cancel."""
     dev = torch.device("cuda")
-    g = torch.Generator(device="cpu").manual_seed(40 + H)
+    g = torch.Generator(device="cpu").manual_seed(40 + H + N)
     C = 64
     L = lib()
     w = (torch.randn(C, 3, 3, C, generator=g) * (9 * C) ** -0.5).to(dev, torch.bfloat16)
     dy = torch.randn(N, H, H, C, generator=g).to(dev, torch.bfloat16)
-    xin = torch.randn(N * H * H, C, generator=g).to(dev, torch.bfloat16)
+    xin = (torch.randn(N * H * H, C, generator=g) + shift).to(dev, torch.bfloat16)
     mean, inv, gamma, beta = _chan(C, dev, g)
+    if shift:  # the BN's own batch statistics of xin
+        mean = xin.float().mean(0)
+        inv = xin.float().var(0, unbiased=False).add(1e-5).rsqrt()
     bits = _pack_mask(xin, mean, inv, gamma, beta)
     gref = torch.nn.grad.conv2d_input((N, C, H, H), w.float().permute(0, 3, 1, 2), dy.permute(0, 3, 1, 2).float(),
                                       padding=1).permute(0, 2, 3, 1).reshape(-1, C)
     dpr, sr, qr = _bwd_ref(gref, xin, mean, inv, gamma, beta)
     outs = []
-    for halo in (1, 0):
+    for halo in (grid, 0):
         L.conv_halo_dgrad_set(halo)
         try:
             dp, part = L.conv_dgrad_bn(dy, w, H, H, 1, 1, xin, mean, inv, gamma, beta, bits=bits)

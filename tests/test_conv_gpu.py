@@ -156,11 +156,12 @@ def test_stem_stream_conv_matches_tiled(N):
     assert _rel(ps[0], yf.sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("N,H", [(3, 56), (2, 28), (2, 30)])
+@pytest.mark.parametrize("N,H", [(3, 56), (2, 28), (2, 30), (40, 56), (75, 28)])
 def test_conv_fwd_bn_halo_64(N, H):
     """conv_fwd_bn for ResNet's stage-1 3x3 (64 -> 64, stride 1, pad 1): H % 4 == 0 runs the direct halo-tile conv
     (csrc/kernels/conv_halo.hip), H = 30 the implicit GEMM; output against the fp32 conv, the BN-statistics partials
-    against the stored output's column sums and sums of squares."""
+    against the stored output's column sums and sums of squares.  N = 40 at 56x56 (560 bands) and N = 75 at 28x28
+    (525 bands) make every persistent workgroup walk 2-3 bands through the double-buffered halo, as at b1024."""
     from dtg.ops._native import lib
     L = lib()
     g = torch.Generator(device="cpu").manual_seed(21 + H)

@@ -190,17 +190,18 @@ def test_allreduce_bw_tool_gloo(tmp_path):
 
 def _rank_step(rank, world, port, q):
     """DataParallel.step (apply per bucket as each all-reduce lands) == finish() + opt.step(), bit for bit, over
-    two steps with momentum (several buckets, the fp32 and compute groups)."""
+    two steps with momentum / Adam / Adagrad (several buckets, the fp32 and compute groups; Adagrad's accumulator
+    must start at 0.1 in every bucket slice, not only the first)."""
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK=str(rank))
         import dtg  # noqa: F401
         from dtg import ops
-        from dtg.optim import FusedAdam, FusedSGD
+        from dtg.optim import FusedAdagrad, FusedAdam, FusedSGD
         from dtg.parallel import DataParallel, FlatParams, comm
         comm.init("gloo")
-        for Opt in (FusedSGD, FusedAdam):
+        for Opt in (FusedSGD, FusedAdam, FusedAdagrad):
             runs = []
             for mode in ("step", "finish"):
                 torch.manual_seed(0)
@@ -224,6 +225,7 @@ def _rank_step(rank, world, port, q):
                             [grp.master.clone() for grp in flat])
                 dp.remove_hooks()
             assert all(torch.equal(a, b) for a, b in zip(*runs)), Opt.__name__
+            assert all(torch.isfinite(t).all() for t in runs[0]), Opt.__name__
         comm.shutdown()
         q.put((rank, "ok"))
     except Exception:  # pragma: no cover - reported to the parent

@@ -1,9 +1,9 @@
 """Lab-extension kernels (dtg._lab, csrc/lab: NOT part of the production _C) against fp32 torch.
 
 These are A/B candidates and negative results kept for the tools (tools/gemm_ab.py, gemm_sweep.py,
-epi_gemm_ab.py, conv_halo_ab.py, gemm5_ab.py): the 256x128 8-wave ring and the rest of the forced tile table
-(gemm_forced*.hip), the 256x256 8-phase GEMM and its persistent form (gemm8.hip), the direct 3x3 halo conv
-(conv_halo.hip), the round-5 main-loop lab (gemm5.hip) and the transposed fused BN dx + weight gradient
+epi_gemm_ab.py, gemm5_ab.py): the 256x128 8-wave ring and the rest of the forced tile table
+(gemm_forced*.hip), the 256x256 8-phase GEMM and its persistent form (gemm8.hip), the round-5 main-loop lab
+(gemm5.hip) and the transposed fused BN dx + weight gradient
 (bn_dxT_wgrad.hip).  Marked ``lab`` (not ``gpu``): the production GPU
 suite does not load the lab extension.  Run with ``python -m pytest tests/test_lab_gpu.py -m lab`` on a GPU box
 after ``python tools/build_ext.py --only lab``.
@@ -86,26 +86,6 @@ def test_gemm_8phase_persistent(M, N, K, b_kc):
     assert _rel(aux, p.grad) < 2e-2
     sav = (torch.rand(M, N, device="cuda") + 0.5).bfloat16()
     assert _rel(_gemm(98, A, True, B, b_kc, aux=sav, aux_mode=4), ref * sav.float()) < 1e-2
-
-
-def test_conv_halo_fwd_matches_fp32_reference():
-    """Direct 3x3 conv from an LDS halo tile (csrc/lab/conv_halo.hip): equals the fp32 convolution, image edges in
-    every band; N = 40 at 56 x 56 gives 560 bands, so the persistent workgroups walk two or three bands each
-    through the double-buffered halo; with the BatchNorm-statistics epilogue."""
-    g = torch.Generator().manual_seed(5)
-    dev = torch.device("cuda")
-    w = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(dev, torch.bfloat16)
-    for n in (3, 40):
-        x = torch.randn(n, 56, 56, 64, generator=g).to(dev, torch.bfloat16)
-        y, _ = _lab().conv_halo_fwd(x, w)
-        ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
-        assert _rel(y, ref) < 1e-2
-        y2, part = _lab().conv_halo_fwd(x, w, True)
-        assert torch.equal(y2, y)
-        p = part.view(-1, 2, 64).sum(0)
-        yf = y.float().reshape(-1, 64)
-        assert ((p[0] - yf.sum(0)).norm() / yf.sum(0).norm()).item() < 1e-3
-        assert ((p[1] - (yf * yf).sum(0)).norm() / (yf * yf).sum(0).norm()).item() < 1e-3
 
 
 @pytest.mark.parametrize("M,N,K", [(2048, 768, 768), (1024, 1536, 3072), (512, 192, 64), (256, 384, 128)])

@@ -6,7 +6,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
     DTG_AB_SET=models.resnet_fused._DXW=0 python tools/bench_cfg.py  # a module switch (dtg.<module>.<name>=<int>)
     DTG_AB_STAGES=0:2,1:3 python tools/bench_cfg.py   # conv LDS schedules per pass (0 fwd, 1 dgrad, 2 wgrad, 3 stem)
     DTG_AB_STEM_STREAM=0 python tools/bench_cfg.py    # the tiled stem conv instead of the streaming one
-    DTG_AB_HALO=1 python tools/bench_cfg.py           # the lab's halo conv for ResNet's stage-1 3x3 forward
+    DTG_AB_HALO=0 python tools/bench_cfg.py           # the implicit-GEMM stage-1 3x3 forward instead of the halo one
     DTG_AB_HALO_DGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 dgrad instead of the halo one
     DTG_AB_HALO_WGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 wgrad instead of the halo one
 """
@@ -20,17 +20,8 @@ sys.path.insert(0, ROOT)
 import dtg  # noqa: E402,F401
 from dtg.ops._native import lib  # noqa: E402
 
-if os.environ.get("DTG_AB_HALO") == "1":  # the lab's direct halo conv for the 64 -> 64 3x3 forward (stage 1)
-    from dtg.ops._native import lab
-    _L, _H = lib(), lab()
-    _orig = _L.conv_fwd_bn
-
-    def _halo_fwd_bn(x, w, stride, pad, pooled=False):
-        if (stride == 1 and pad == 1 and x.shape[-1] == 64 and tuple(w.shape) == (64, 3, 3, 64)
-                and w.is_contiguous() and x.is_contiguous() and x.shape[1] % 4 == 0):
-            return _H.conv_halo_fwd(x, w, True)
-        return _orig(x, w, stride, pad, pooled=pooled)
-    _L.conv_fwd_bn = _halo_fwd_bn
+if os.environ.get("DTG_AB_HALO"):  # 0: the implicit-GEMM forward for the stage-1 3x3 (conv_halo.hip EPI 0)
+    lib().conv_halo_fwd_set(int(os.environ["DTG_AB_HALO"]))
 if os.environ.get("DTG_AB_STEM_STREAM"):  # 0: the tiled stem conv instead of the streaming one
     lib().stem_stream_set(int(os.environ["DTG_AB_STEM_STREAM"]))
 if os.environ.get("DTG_AB_HALO_DGRAD"):  # 0: the implicit-GEMM dgrad for the stage-1 3x3 (conv_halo.hip EPI 1)
