@@ -16,7 +16,7 @@ __version__ = "0.1.0"
 
 from .graph import (GraphKeys, Graph, Tensor, Op, get_default_graph, reset_default_graph,  # noqa: F401
                     add_to_collection, get_collection, get_collection_ref, control_dependencies, name_scope,
-                    device, constant, no_op, group, identity, convert_to_tensor, square, abs, sqrt, exp, log,
+                    device, constant, placeholder, no_op, group, identity, convert_to_tensor, square, abs, sqrt, exp, log,
                     relu, tanh, reduce_mean, reduce_sum, reduce_max, matmul)
 from .variables import (Variable, get_variable, assign, assign_add, global_variables, local_variables,  # noqa: F401
                         trainable_variables, all_variables, variables_initializer, global_variables_initializer,

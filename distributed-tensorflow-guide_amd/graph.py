@@ -390,6 +390,16 @@ def constant(value, shape=None, dtype=torch.float32, name="Const"):
     return Tensor(lambda c: t, [], name)
 
 
+def placeholder(dtype=None, shape=None, name="Placeholder"):
+    """tf.placeholder: a value supplied through ``feed_dict`` at run time.  Fed torch tensors are used as they
+    are (a GPU batch stays on the GPU), so an eager train step (dtg.train.eager) takes its batch this way."""
+    def run(ctx):
+        raise ValueError("You must feed a value for placeholder tensor '%s'" % t._name)
+    t = Tensor(run, [], name)
+    t.dtype, t.shape = dtype, shape
+    return t
+
+
 def no_op(name="NoOp"):
     return Op(lambda c: None, [], name)
 

@@ -20,6 +20,11 @@ class _FlatOptimizer:
         self.wd_groups = set(wd_groups)
         self.step_count = 0
 
+    def new_slot(self, g, key):
+        """Allocate (and initialise) group ``g``'s optimizer slot ``key`` -- also its alignment padding, which no
+        checkpoint holds (a restore allocates the slots it loads through this)."""
+        return g.state_buffer(key)
+
     def set_lr(self, lr):
         self.lr = float(lr)
         self.hyper[0].fill_(self.lr)
@@ -47,6 +52,13 @@ class _FlatOptimizer:
                 for g, lo, hi, ready in ranges:
                     ready()
                     self._apply(_Slice(g, lo, hi), grad_scale, zero_grad)
+
+    def minimize(self, loss_fn, global_step=None, inputs=(), name=None):
+        """A train op for dtg sessions (``sess.run(op, feed_dict)``): forward + backward of ``loss_fn(*inputs)``,
+        this optimizer's fused apply, global_step += 1, on one replica (train/eager.py; for several ranks wrap it
+        in ``dtg.train.SyncReplicasOptimizer``, the all-reduce mode)."""
+        from ..train.eager import minimize
+        return minimize(self, loss_fn, global_step, inputs, None, name)
 
     def state_dict(self):
         return {"step": self.step_count, "lr": self.lr,
@@ -114,13 +126,20 @@ class FusedAdagrad(_FlatOptimizer):
         self.init_acc = initial_accumulator_value
         self.eps = eps
 
+    def new_slot(self, g, key):
+        fresh = key not in g.state
+        buf = g.state_buffer(key)
+        if fresh and key == "acc":
+            buf.fill_(self.init_acc)
+        return buf
+
     def _acc(self, g):
         # the WHOLE group's accumulator is created and filled with the initial value on first use: DataParallel.step
         # applies a group slice by slice (_Slice shares the group's state dict), so a per-slice "fresh" test would
         # fill only the first slice and leave later slices at the allocator's zeros (lr * sign(g), or 0/0)
         full = g._g if isinstance(g, _Slice) else g
         if "acc" not in full.state:
-            full.state_buffer("acc").fill_(self.init_acc)
+            self.new_slot(full, "acc")
         return g.state_buffer("acc")
 
     def _apply(self, g, gscale, zero_grad):

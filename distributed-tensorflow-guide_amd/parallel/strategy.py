@@ -10,26 +10,43 @@ for N > 1, a no-op reducer for N = 1), exposed with the TF names a user of the g
     trainer = strategy.distribute(model, lambda flat: FusedSGD(flat, lr=0.05))
     for x, y in data:
         loss = trainer.step(lambda: loss_fn(model(x), y))
+
+or, session-driven (hooks, checkpoints, resume -- train/eager.py)::
+
+    x, y = dtg.placeholder(), dtg.placeholder()
+    train_op = trainer.minimize(lambda x, y: loss_fn(model(x), y), global_step=gs, inputs=(x, y))
+    with dtg.train.MonitoredTrainingSession(is_chief=strategy.rank == 0, checkpoint_dir=ck,
+                                            hooks=[trainer.make_session_run_hook(strategy.rank == 0), ...]) as sess:
+        while not sess.should_stop():
+            sess.run(train_op, feed_dict={x: xb, y: yb})
+
+Both run ``DataParallel.step``: each bucket's fused apply as soon as its all-reduce has landed.  The trainer
+is the all-reduce mode of ``dtg.train.SyncReplicasOptimizer`` (replicas_to_aggregate = total = world).
 """
 import contextlib
 
 import torch
 
 from . import comm
-from .ddp import DataParallel
 from .flat import FlatParams
 
 
 class _Trainer:
-    def __init__(self, flat, dp, opt):
-        self.flat, self.dp, self.opt = flat, dp, opt
+    def __init__(self, flat, sro):
+        self.flat, self.sro = flat, sro
+        self.dp, self.opt = sro.dp, sro._flat_opt
 
     def step(self, loss_fn):
         loss = loss_fn()
         loss.backward()
-        self.dp.finish()
-        self.opt.step(grad_scale=self.dp.grad_scale)
+        self.dp.step(self.opt)  # per-bucket apply overlapped with the collective tail
         return loss
+
+    def minimize(self, loss_fn, global_step=None, inputs=(), name=None):
+        return self.sro.minimize(loss_fn, global_step=global_step, inputs=inputs, name=name)
+
+    def make_session_run_hook(self, is_chief):
+        return self.sro.make_session_run_hook(is_chief)
 
 
 class MirroredStrategy:
@@ -52,10 +69,14 @@ class MirroredStrategy:
             yield self
 
     def distribute(self, model, optimizer_fn):
+        from ..train.saver import register_flat_model
+        from ..train.sync_replicas import SyncReplicasOptimizer
         flat = FlatParams(model, compute_dtype=self.compute_dtype)
-        dp = DataParallel(flat, bucket_mb=self.bucket_mb)
-        dp.broadcast_parameters(0)
-        return _Trainer(flat, dp, optimizer_fn(flat))
+        sro = SyncReplicasOptimizer(optimizer_fn(flat), self.world, self.world, bucket_mb=self.bucket_mb)
+        sro._check_allreduce()
+        sro._data_parallel().broadcast_parameters(0)
+        register_flat_model(flat, sro._flat_opt)  # Saver / CheckpointSaverHook keys: the parameter names
+        return _Trainer(flat, sro)
 
     def shard(self, t):
         """This replica's slice of a global batch (dim 0)."""

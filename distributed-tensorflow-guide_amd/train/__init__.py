@@ -11,7 +11,10 @@ from .hooks import (SessionRunHook, SessionRunArgs, SessionRunContext, SessionRu
 from .session import (MonitoredTrainingSession, MonitoredSession, Supervisor, Scaffold, SessionManager,  # noqa: F401
                       Coordinator, ChiefSessionCreator, WorkerSessionCreator, Session)
 from .saver import (Saver, latest_checkpoint, get_checkpoint_state, update_checkpoint_state,  # noqa: F401
-                    checkpoint_exists, CheckpointReader, load_checkpoint, save_flat, restore_flat)
+                    checkpoint_exists, CheckpointReader, load_checkpoint, save_flat, restore_flat,
+                    register_flat_model, flat_arrays)
+from .eager import broadcast_training_state  # noqa: F401
+from . import eager  # noqa: F401
 from .summary import FileWriter  # noqa: F401
 
 NewCheckpointReader = CheckpointReader

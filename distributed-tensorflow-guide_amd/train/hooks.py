@@ -140,14 +140,24 @@ class LoggingTensorHook(SessionRunHook):
 
 
 class StepCounterHook(SessionRunHook):
-    """global_step/sec (and examples/sec when ``batch_size`` is given) to stdout, a JSONL metrics
-    file and the TF event file of ``output_dir``."""
+    """global_step/sec (and examples/sec when ``batch_size`` is given) to a JSONL metrics file, the TF event
+    file of ``output_dir`` and, with ``log``, stdout.
+
+    For eager GPU steps the host runs ahead of the device, so with ``sync_device`` (default: when CUDA is
+    initialised) the hook synchronises the device at each report -- only then, every ``every_n_steps`` steps --
+    and the rate is the device's.  ``aggregate=True`` (all-reduce data parallelism: every rank runs the hook at
+    the same global steps) sums the per-worker examples/sec over the process group at each report, so each
+    record carries ``examples/sec`` (this worker) and ``examples/sec/node`` (the whole job); that is a
+    collective, so it needs step-based reporting (``every_n_secs`` is refused with it)."""
 
     def __init__(self, every_n_steps=100, every_n_secs=None, output_dir=None, summary_writer=None, batch_size=None,
-                 metrics_path=None):
+                 metrics_path=None, aggregate=False, sync_device=None, log=False, process_group=None):
+        if aggregate and every_n_secs is not None:
+            raise ValueError("StepCounterHook(aggregate=True) reports at fixed steps: use every_n_steps")
         self._n, self._secs = every_n_steps, every_n_secs
         self._dir, self._writer, self._bs = output_dir, summary_writer, batch_size
         self._metrics = metrics_path
+        self._aggregate, self._sync, self._log, self._pg = aggregate, sync_device, log, process_group
         self._last_step, self._last_t = None, None
         self.history = []
 
@@ -160,30 +170,70 @@ class StepCounterHook(SessionRunHook):
     def before_run(self, run_context):
         return SessionRunArgs(self._gs) if self._gs is not None else None
 
+    def _device_sync(self):
+        sync = self._sync
+        try:
+            import torch
+            if sync is None:
+                sync = torch.cuda.is_available() and torch.cuda.is_initialized()
+            if sync:
+                torch.cuda.synchronize()
+        except Exception:  # noqa: BLE001 - a CPU-only build
+            pass
+
+    def _node_total(self, eps):
+        try:
+            import torch
+            import torch.distributed as dist
+        except Exception:  # noqa: BLE001
+            return eps, 1
+        if not (dist.is_available() and dist.is_initialized()):
+            return eps, 1
+        w = dist.get_world_size(self._pg)
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self._pg) == "nccl" \
+            else torch.device("cpu")
+        t = torch.tensor([float(eps)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, group=self._pg)
+        return float(t.item()), w
+
     def after_run(self, run_context, run_values):
         if run_values.results is None:
             return
-        step, now = int(run_values.results), time.time()
+        step = int(run_values.results)
         if self._last_step is None:
-            self._last_step, self._last_t = step, now
+            self._device_sync()
+            self._last_step, self._last_t = step, time.time()
             return
-        due = (self._secs is not None and now - self._last_t >= self._secs) or \
+        due = (self._secs is not None and time.time() - self._last_t >= self._secs) or \
               (self._secs is None and step - self._last_step >= (self._n or 1))
         if not due:
             return
+        self._device_sync()
+        now = time.time()
         dt = max(now - self._last_t, 1e-9)
         sps = (step - self._last_step) / dt
         rec = {"step": step, "global_step/sec": sps, "time": now}
         if self._bs:
             rec["examples/sec"] = sps * self._bs
+            if self._aggregate:
+                rec["examples/sec/node"], rec["workers"] = self._node_total(rec["examples/sec"])
         self.history.append(rec)
         if self._writer is not None:
             self._writer.add_scalar("global_step/sec", sps, step)
             if self._bs:
                 self._writer.add_scalar("examples/sec", sps * self._bs, step)
+                if "examples/sec/node" in rec:
+                    self._writer.add_scalar("examples/sec/node", rec["examples/sec/node"], step)
         if self._metrics:
             with open(self._metrics, "a") as f:
                 f.write(json.dumps(rec) + "\n")
+        if self._log:
+            msg = "global_step/sec: %.4g" % sps
+            if self._bs:
+                msg += ", examples/sec: %.6g" % rec["examples/sec"]
+                if "examples/sec/node" in rec:
+                    msg += " (node %.6g over %d workers)" % (rec["examples/sec/node"], rec["workers"])
+            print(msg, flush=True)
         self._last_step, self._last_t = step, now
 
 

@@ -178,7 +178,16 @@ class Saver:
                 for n, a in zip(names, c.read(names) if names else []):
                     arrays.append((n, a))
                     seen.add(n)
+        for fm in self._flat_models():  # eager GPU models (register_flat_model): parameter-name keys
+            for n, a in fm.arrays():
+                if n in seen:
+                    raise ValueError("checkpoint key %r is both a graph variable and a model parameter" % n)
+                arrays.append((n, a))
+                seen.add(n)
         return arrays
+
+    def _flat_models(self):
+        return G.get_collection(FLAT_MODELS) if self._var_list is None else []
 
     def save(self, sess, save_path, global_step=None, latest_filename=None, meta_graph_suffix="meta",
              write_meta_graph=True, write_state=True):
@@ -213,6 +222,9 @@ class Saver:
     def restore(self, sess, save_path):
         vals = read_tensors(save_path)
         restored = []
+        for fm in self._flat_models():
+            fm.restore(vals, save_path)
+            restored.extend(fm.names())
         by_name = dict(zip(self._names(), self._vars()))
         tasks = set()
         for name, v in by_name.items():
@@ -238,10 +250,45 @@ class Saver:
 
 
 # ---- flat-buffer models ---------------------------------------------------------------------
+FLAT_MODELS = "dtg_flat_models"  # graph collection of _FlatModel saveables (Saver / CheckpointSaverHook)
+
+
+class _FlatModel:
+    """A FlatParams model (and its fused optimizer) as a Saver saveable: the same keys as :func:`save_flat`."""
+
+    def __init__(self, flat, optimizer=None):
+        self.flat, self.optimizer = flat, optimizer
+
+    def arrays(self):
+        return flat_arrays(self.flat, self.optimizer)
+
+    def names(self):
+        return [n for n, _ in self.flat.named_masters()]
+
+    def restore(self, vals, what="checkpoint"):
+        load_flat_arrays(self.flat, vals, self.optimizer, None, what)
+
+
+def register_flat_model(flat, optimizer=None):
+    """Make ``Saver()`` (and so MonitoredTrainingSession's CheckpointSaverHook and its restore) checkpoint a
+    FlatParams model: one key per parameter name, its buffers, and the optimizer's slots and step.  Idempotent
+    per ``flat``; a later call with an optimizer attaches it."""
+    for fm in G.get_collection(FLAT_MODELS):
+        if fm.flat is flat:
+            if optimizer is not None:
+                fm.optimizer = optimizer
+            return fm
+    fm = _FlatModel(flat, optimizer)
+    G.add_to_collection(FLAT_MODELS, fm)
+    return fm
+
+
 SLOT_LAYOUT_KEY = "dtg/slot_layout"
 SLOT_LAYOUT_LOGICAL = 1
-def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_dir=None, optimizer=None):
-    """Checkpoint a FlatParams model (+ module buffers, optimizer state) as a TensorBundle."""
+def flat_arrays(flat, optimizer=None):
+    """The named fp32 arrays of a FlatParams model -- one key per parameter (its module name), the module's
+    buffers, and with ``optimizer`` its slots as ``<param>/<slot>`` plus ``optimizer/step`` -- as written by
+    :func:`save_flat` and by :class:`Saver` for models registered with ``dtg.train.register_flat_model``."""
     arrays = [(n, _np_of(v)) for n, v in flat.named_masters()]
     for n, b in flat.module.named_buffers():
         arrays.append((n, _np_of(b)))
@@ -257,6 +304,12 @@ def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_d
                     # same logical layout as the master (channels_last conv weights included), so
                     # '<param>/<slot>' is element-aligned with '<param>' for any reader
                     arrays.append(("%s/%s" % (n, k), _np_of(_view_like(buf, g.offsets[i], g.params[i]))))
+    return arrays
+
+
+def save_flat(flat, prefix, global_step=None, extra=None, max_to_keep=5, state_dir=None, optimizer=None):
+    """Checkpoint a FlatParams model (+ module buffers, optimizer state) as a TensorBundle."""
+    arrays = flat_arrays(flat, optimizer)
     if global_step is not None:
         arrays.append(("global_step", np.array(int(global_step), dtype=np.int64)))
         prefix = "%s-%d" % (prefix, int(global_step))
@@ -285,22 +338,32 @@ def restore_flat(flat, prefix, optimizer=None, legacy_slot_layout=None):
     the ``dtg/slot_layout`` marker (added later).  Only checkpoints from before f74dff1 hold channels_last
     conv slots in physical [K,R,S,C] order; converting those is opt-in (``legacy_slot_layout=True`` or
     ``DTG_LEGACY_SLOT_LAYOUT=1``), and refused for a checkpoint that carries the logical marker."""
-    from ..parallel.flat import _view_like
     vals = read_tensors(prefix)
+    load_flat_arrays(flat, vals, optimizer, legacy_slot_layout, prefix)
+    return int(vals["global_step"]) if "global_step" in vals else None
+
+
+def load_flat_arrays(flat, vals, optimizer=None, legacy_slot_layout=None, what="checkpoint"):
+    """Load the arrays :func:`flat_arrays` produced (a dict name -> ndarray) into ``flat`` (and ``optimizer``)."""
+    from ..parallel.flat import _view_like
     if legacy_slot_layout is None:
         legacy_slot_layout = os.environ.get("DTG_LEGACY_SLOT_LAYOUT") == "1"
     marked = int(vals.get(SLOT_LAYOUT_KEY, -1)) == SLOT_LAYOUT_LOGICAL
     if legacy_slot_layout and marked:
-        raise ValueError("%s: legacy_slot_layout requested, but the checkpoint is marked logical" % prefix)
+        raise ValueError("%s: legacy_slot_layout requested, but the checkpoint is marked logical" % what)
     logical = not legacy_slot_layout
     with torch.no_grad():
         for g in flat:
             if optimizer is not None:  # slots present in the checkpoint but not yet allocated
                 for n in g.names:
                     for key in vals:
-                        if key.startswith(n + "/") and "/" not in key[len(n) + 1:]:
-                            g.state_buffer(key[len(n) + 1:])
+                        if key.startswith(n + "/") and "/" not in key[len(n) + 1:] and key[len(n) + 1:] not in g.state:
+                            k = key[len(n) + 1:]
+                            # the optimizer initialises what the checkpoint does not hold (alignment padding)
+                            optimizer.new_slot(g, k) if hasattr(optimizer, "new_slot") else g.state_buffer(k)
             for i, n in enumerate(g.names):
+                if n not in vals:
+                    raise KeyError("Key %s not found in %s" % (n, what))
                 mv = g.master_view(i)
                 mv.copy_(torch.from_numpy(vals[n]).view(mv.shape))
                 for k, buf in g.state.items():
@@ -322,4 +385,3 @@ def restore_flat(flat, prefix, optimizer=None, legacy_slot_layout=None):
         optimizer.step_count = int(vals["optimizer/step"])
         if hasattr(optimizer, "hyper"):
             optimizer.hyper[1].fill_(float(optimizer.step_count))
-    return int(vals["global_step"]) if "global_step" in vals else None

@@ -290,6 +290,13 @@ class _MonitoredSession(_Session):
                 self._recreate()
 
 
+def _ps_backed():
+    """Does any global variable live on a parameter server?  Without one (all-reduce data parallelism, eager
+    models) a non-chief has nothing to wait for: it initialises its own variables, and the sync hook gives it
+    the chief's state (train/eager.py broadcast_training_state)."""
+    return any(getattr(v, "remote", False) for v in G.get_collection(G.GraphKeys.GLOBAL_VARIABLES))
+
+
 def _make_recreate(sess, sm, scaffold, checkpoint_dir, is_chief, hooks, timeout):
     def recreate():
         close_connections()
@@ -300,6 +307,8 @@ def _make_recreate(sess, sm, scaffold, checkpoint_dir, is_chief, hooks, timeout)
         if is_chief:
             sm.prepare_session(sess, scaffold.init_op, scaffold.saver, checkpoint_dir, scaffold.init_fn,
                                scaffold.init_feed_dict)
+        elif not _ps_backed():
+            sm.prepare_session(sess, scaffold.init_op, None, None, scaffold.init_fn, scaffold.init_feed_dict)
         else:
             sm.wait_for_session(sess, timeout)
         print("[dtg] session recovered%s" % (" from " + sess.restored_from if sess.restored_from else ""),
@@ -338,6 +347,8 @@ def MonitoredTrainingSession(master="", is_chief=True, checkpoint_dir=None, scaf
     if is_chief:
         sm.prepare_session(sess, scaffold.init_op, scaffold.saver, checkpoint_dir, scaffold.init_fn,
                            scaffold.init_feed_dict)
+    elif not _ps_backed():
+        sm.prepare_session(sess, scaffold.init_op, None, None, scaffold.init_fn, scaffold.init_feed_dict)
     else:
         sm.wait_for_session(sess, max_wait_secs)
     for h in all_hooks:

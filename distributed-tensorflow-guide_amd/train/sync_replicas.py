@@ -12,9 +12,20 @@ Two execution modes behind one API:
   M - N gradients per step are backups and get dropped (Synchronous-SGD/README.md:3).
   Native pieces: csrc/ps/server.cc ACC_* and Q_* ops.
 
-* **All-reduce mode** (``dtg.parallel.DataParallel``): no PS, one gradient per rank, bucketed RCCL
-  all-reduce overlapped with backward -- the fast path for the north-star models.  See
-  ``SyncReplicasOptimizer.allreduce()``.
+* **All-reduce mode** (no PS and ``replicas_to_aggregate == total_num_replicas`` == the process-group size): one
+  gradient per rank, summed by RCCL (gloo on CPU) and averaged, so every replica applies the same update --
+  what the accumulator computes when nobody is stale, without the PS round trips.  Two forms:
+
+  - eager GPU models: the wrapped optimizer is a fused flat optimizer (``dtg.optim``) -- or a tf.train
+    optimizer plus ``var_list=<FlatParams>`` -- and ``minimize(loss_fn, global_step, inputs=...)`` takes a
+    callable.  The train op is forward + backward with bucketed all-reduces fired from inside the backward,
+    then ``DataParallel.step`` (each bucket applied as its collective lands; train/eager.py);
+  - graph variables that are not on a PS (the toy graph): ``apply_gradients`` all-reduces each gradient and
+    applies the wrapped optimizer locally on every replica.
+
+  ``make_session_run_hook`` broadcasts the chief's state (restored from a checkpoint, or freshly initialised)
+  to every rank once the session exists.  Backup workers (R < M) need the accumulator: all-reduce has no
+  stale gradient to drop, so that combination is refused.
 """
 import os
 import threading
@@ -34,9 +45,16 @@ TOKEN_QUEUE = "sync_token_q"
 
 class SyncReplicasOptimizer(Optimizer):
     def __init__(self, opt, replicas_to_aggregate, total_num_replicas=None, variable_averages=None,
-                 variables_to_average=None, use_locking=False, name="sync_replicas"):
-        super().__init__(opt._lr, use_locking, name)
+                 variables_to_average=None, use_locking=False, name="sync_replicas", bucket_mb=25.0,
+                 process_group=None):
+        from .eager import is_flat_optimizer
+        super().__init__(opt.lr if is_flat_optimizer(opt) else opt._lr, use_locking, name)
         self._opt = opt
+        self._bucket_mb = float(bucket_mb)
+        self._pg = process_group
+        self.dp = None              # all-reduce mode over a FlatParams model: its DataParallel
+        self.mode = None            # "ps" | "allreduce" (decided when the train op is built)
+        self._flat_opt = opt if is_flat_optimizer(opt) else None
         self._replicas_to_aggregate = int(replicas_to_aggregate)
         self._total_num_replicas = int(total_num_replicas or replicas_to_aggregate)
         self._tokens_per_step = max(self._total_num_replicas, self._replicas_to_aggregate)
@@ -62,6 +80,51 @@ class SyncReplicasOptimizer(Optimizer):
             task = s.task_index if s is not None else 0
         return "%s/%d" % (TOKEN_QUEUE, task)
 
+    # ---- all-reduce mode ------------------------------------------------------------------------
+    def _world(self):
+        import torch.distributed as dist
+        return dist.get_world_size(self._pg) if dist.is_available() and dist.is_initialized() else 1
+
+    def _check_allreduce(self):
+        if self._replicas_to_aggregate != self._total_num_replicas:
+            raise ValueError(
+                "replicas_to_aggregate=%d < total_num_replicas=%d (backup workers) needs the PS-accumulator mode: "
+                "all-reduce has no stale gradient to drop -- place the variables on a PS (replica_device_setter)"
+                % (self._replicas_to_aggregate, self._total_num_replicas))
+        w = self._world()
+        if self._total_num_replicas != w:
+            raise ValueError("all-reduce mode: total_num_replicas=%d but the process group has %d rank(s) (one "
+                             "replica per process)" % (self._total_num_replicas, w))
+        self.mode = "allreduce"
+
+    def _flat_for(self, var_list):
+        from ..parallel.flat import FlatParams
+        from .eager import fused_from_tf
+        if self._flat_opt is None:
+            if not isinstance(var_list, FlatParams):
+                raise TypeError("an eager train op wraps a fused flat optimizer (dtg.optim) or gets "
+                                "var_list=<FlatParams> for a tf.train optimizer")
+            self._flat_opt = fused_from_tf(self._opt, var_list)
+        return self._flat_opt
+
+    def _data_parallel(self):
+        if self.dp is None:
+            from ..parallel.ddp import DataParallel
+            self.dp = DataParallel(self._flat_opt.flat, process_group=self._pg, bucket_mb=self._bucket_mb)
+        return self.dp
+
+    def minimize(self, loss, global_step=None, var_list=None, name=None, inputs=()):
+        """``loss`` callable (an eager model's ``loss_fn(*inputs)``): the all-reduce train op of train/eager.py.
+        Otherwise the graph form: compute_gradients + apply_gradients."""
+        if not callable(loss) or isinstance(loss, G.Node):
+            return super().minimize(loss, global_step=global_step, var_list=var_list, name=name)
+        self._flat_for(var_list)
+        self._check_allreduce()
+        self._global_step = global_step
+        from .eager import minimize as eager_minimize
+        return eager_minimize(self._flat_opt, loss, global_step, inputs, self._data_parallel(),
+                              name or "sync_replicas_train")
+
     # ------------------------------------------------------------------------------------------
     def compute_gradients(self, *args, **kwargs):
         return self._opt.compute_gradients(*args, **kwargs)
@@ -71,10 +134,13 @@ class SyncReplicasOptimizer(Optimizer):
             raise ValueError("SyncReplicasOptimizer.apply_gradients needs global_step")
         self._gv = [(g, v) for g, v in grads_and_vars]
         self._global_step = global_step
-        for _, v in self._gv:
-            if not (isinstance(v, Variable) and v.remote):
-                raise ValueError("PS-accumulator mode needs variables on a parameter server; for PS-less "
-                                 "synchronous training use dtg.parallel.DataParallel (all-reduce mode)")
+        remote = [isinstance(v, Variable) and v.remote for _, v in self._gv]
+        if not any(remote):
+            self._check_allreduce()
+            return _AllReduceTrainOp(self, name or "sync_replicas_train")
+        if not all(remote):
+            raise ValueError("SyncReplicasOptimizer: some variables are on a parameter server and some are not")
+        self.mode = "ps"
         self.chief_init_op = Op(lambda c: self._init_local_step(), [], "sync_rep_local_step_init")
         self.local_step_init_op = self.chief_init_op
         self.ready_for_local_init_op = _ReadyForLocalInit(self)
@@ -114,6 +180,8 @@ class SyncReplicasOptimizer(Optimizer):
         return Op(run, [], "sync_replicas/init_tokens")
 
     def make_session_run_hook(self, is_chief, num_tokens=-1):
+        if self.mode == "allreduce":
+            return _AllReduceSyncHook(self, is_chief)
         return _SyncReplicasHook(self, is_chief, num_tokens)
 
     # ---- chief aggregation loop (TF: get_chief_queue_runner) ---------------------------------
@@ -252,3 +320,77 @@ class _SyncReplicasHook(SessionRunHook):
     def end(self, session):
         if self._is_chief:
             self._sro.stop_chief()
+
+
+class _AllReduceTrainOp(Op):
+    """All-reduce mode for graph variables that live on the workers: every replica evaluates its gradients, they
+    are summed over the process group and averaged, and every replica applies the wrapped optimizer's rule
+    locally -- the same update on every rank, one global step per run."""
+
+    def __init__(self, sro, name):
+        self.sro = sro
+        super().__init__(lambda c: None, [g for g, _ in sro._gv], name)
+
+    def _eval(self, ctx):
+        import torch.distributed as dist
+        sro = self.sro
+        opt = sro._opt
+        grads = [ctx.eval(g) for g, _ in sro._gv]
+        w = sro._world()
+        if w > 1:
+            # one flat fp32 buffer: a single collective per step
+            flat = torch.cat([g.detach().float().reshape(-1) for g in grads])
+            dist.all_reduce(flat, group=sro._pg)
+            flat /= w
+            out, off = [], 0
+            for g in grads:
+                out.append(flat[off:off + g.numel()].view(g.shape))
+                off += g.numel()
+            grads = out
+        lr = opt._lr_value(ctx)
+        opt._t += 1
+        for g, (_, v) in zip(grads, sro._gv):
+            if g is not None:
+                opt._apply_local(v, g, lr)
+        gs = sro._global_step
+        with gs._lock:
+            gs._local.add_(1)
+        return None
+
+
+class _AllReduceSyncHook(SessionRunHook):
+    """All-reduce mode: once the session exists (the chief has restored its checkpoint or initialised), every
+    rank takes the chief's parameters, buffers, optimizer state and global step -- TF's chief-init + token
+    rendezvous collapsed into one broadcast."""
+
+    def __init__(self, sro, is_chief):
+        self._sro = sro
+        self._is_chief = is_chief
+
+    def after_create_session(self, session, coord):
+        sro = self._sro
+        if sro._world() == 1:
+            return
+        if sro._flat_opt is not None and sro.dp is not None:
+            from .eager import broadcast_training_state
+            broadcast_training_state(sro._flat_opt.flat, sro._flat_opt, sro.dp, sro._global_step, 0, sro._pg)
+            return
+        import torch.distributed as dist
+        for _, v in sro._gv:
+            t = v.read_value()
+            dist.broadcast(t, 0, group=sro._pg)
+        for s in _slot_tensors(sro._opt, [v for _, v in sro._gv]):
+            dist.broadcast(s, 0, group=sro._pg)
+        gs = sro._global_step
+        t = gs.read_value()
+        dist.broadcast(t, 0, group=sro._pg)
+
+
+def _slot_tensors(opt, vars_):
+    out = []
+    for v in vars_:
+        for k in opt.get_slot_names():
+            s = opt.get_slot(v, k)
+            if isinstance(s, torch.Tensor):
+                out.append(s)
+    return out
