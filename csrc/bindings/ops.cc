@@ -947,6 +947,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_halo_fwd_set", [](int64_t on) { dtg::conv3x3_halo_fwd_set((int)on); });
   m.def("conv_halo_dgrad_set", [](int64_t on) { dtg::conv3x3_halo_dgrad_set((int)on); });
   m.def("conv_halo_wgrad_set", [](int64_t on) { dtg::conv3x3_halo_wgrad_set((int)on); });
+  m.def("conv_lin_wgrad_set", [](int64_t on) { dtg::conv3x3_lin_wgrad_set((int)on); });
   m.def("hyper_tick", [](Tensor hyper) {
     check_hyper(hyper);
     c10::DeviceGuard dg(hyper.device());

@@ -264,7 +264,13 @@ void conv3x3_halo_dgrad_set(int on);  // (A/B tools) the halo data gradient on /
 // its weight gradient (W = 56): the split (= workgroups, one fp32 slab each) conv_wgrad uses, 0 if not this shape
 int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w);
 void conv3x3_halo_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int grid, int N, int H, hipStream_t st);
-void conv3x3_halo_wgrad_set(int on);  // (A/B tools) the halo weight gradient on / off
+void conv3x3_halo_wgrad_set(int on);
+// linear-halo 3x3 weight gradient (conv_halo.hip) for 7x7 / 14x14 / 28x28 layers with C, K multiples of 64: split =
+// band ranges (split-K slabs), 0 when the shape is not covered
+int conv3x3_lin_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w);
+void conv3x3_lin_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int split, int N, int H, int W, int C, int K,
+                       hipStream_t st);
+void conv3x3_lin_wgrad_set(int on);  // (A/B tools) on / off  // (A/B tools) the halo weight gradient on / off
 void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int K, int R, int S,
               int stride, int pad, hipStream_t st, const BnEpi& bn = BnEpi());
 // returns 0 if bn.mode != 0 was asked for a geometry the fused statistics cannot cover (strided dgrad

@@ -620,6 +620,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
 int conv_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w,
                      int target_wgs) {
   if (int hs = conv3x3_halo_wgrad_split(N, H, W, C, K, R, S, stride, pad, stride_w)) return hs;  // conv_halo.hip
+  if (int ls = conv3x3_lin_wgrad_split(N, H, W, C, K, R, S, stride, pad, stride_w)) return ls;
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad, stride_w);
   const int M = N * G.P * G.Q, No = R * S * C;
   const long long tiles = K <= 64 ? (long long)((No + 255) / 256) : (long long)((K + 127) / 128) * ((No + 127) / 128);
@@ -640,6 +641,11 @@ void conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float 
                 int sched) {
   if (split == conv3x3_halo_wgrad_split(N, H, W, C, K, R, S, stride, pad, stride_w)) {  // stage-1 3x3: halo tiles
     conv3x3_halo_wgrad(dy, x, ws, split, N, H, st);
+    gemm_splitk_reduce(ws, split, K, R * S * C, Epi{dw, R * S * C, dw_bf16, 1.f, beta, nullptr, 0}, st);
+    return;
+  }
+  if (split == conv3x3_lin_wgrad_split(N, H, W, C, K, R, S, stride, pad, stride_w)) {  // stages 2-4: linear halo
+    conv3x3_lin_wgrad(dy, x, ws, split, N, H, W, C, K, st);
     gemm_splitk_reduce(ws, split, K, R * S * C, Epi{dw, R * S * C, dw_bf16, 1.f, beta, nullptr, 0}, st);
     return;
   }

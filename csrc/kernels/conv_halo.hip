@@ -439,6 +439,208 @@ __global__ void __launch_bounds__(256) conv3x3_halo_wgrad_kernel(const bf16_t* _
         slab[(i * 16 + g * 4 + r) * (9 * kC) + (9 * wave + j) * 16 + (lane & 15)] = acc[i][j][r];
 }
 
+// Linear-halo weight gradient for any 3x3 / s1 / p1 layer with C, K multiples of 64 (ResNet-50 stages 2-4: 28x28 x 128,
+// 14x14 x 256, 7x7 x 512).  The whole batch is laid out as one tall virtual image: each image row padded with zero
+// columns to a pitch HP (a multiple of 8 >= W + 1) and each image followed by one zero row (VR = H + 1 rows per
+// image); the pad column / row doubles as the next row's left halo / the next image's top halo.  Output position
+// p = (img * VR + oh) * HP + ow (dy = 0 on the pad) then reads tap (dr, ds) of x at the SAME linear index plus
+// dr * HP + ds, so a band of BP = 256 consecutive positions needs the x rows [p0, p0 + BP + 2 HP + 2): the halo
+// costs 2 HP + 2 rows per band (1.14-1.38x x reads; stage 1's kernel re-reads 2 of every 4 image rows) and no read
+// address needs a division.  Every fragment row is 32 st + (a per-lane constant), so each transposed read is buffer
+// base + st * 4096 + a per-lane table entry (the swizzle of a row depends on row & 15 only): no address VALU in
+// the MFMA loop.
+// Staging: a wave's 64 lanes move 8 consecutive positions x 8 16-byte chunks, and with HP a multiple of 8 those 8
+// positions never straddle a virtual row -- so the row, image and their validity are wave-uniform (SALU), and a
+// chunk costs ~4 VALU (the column check and a buffer offset; out-of-range offsets read 0 through the buffer
+// descriptor's range check).  The first version decomposed every position per lane (~800 VALU per band, 36 % of the
+// wave cycles, profiles/r06_lin_wgrad).  The next band's chunks are loaded in the band's first 3 steps and written
+// to the other buffer in its last 3 (5 steps of MFMAs hide the load latency).
+// Work split: a workgroup owns one 64 (k) x 576 (tap, c) block of dW -- channel blocks (kb, cb), the stage-1
+// accumulator layout -- over a contiguous run of bands; the (kb, cb) pairs of one band range sit on the same XCD
+// (they read the same dy / x rows through its L2).  One fp32 slab per band range, summed by the split-K reduce.
+// Pad positions: 1 - HW / (VR HP) = 16 % (28x28), 18 % (14x14), 23 % (7x7) of the MFMAs.
+template <int W, int H>
+struct LinGeom {
+  static constexpr int HP = (W + 1 + 7) / 8 * 8, VR = H + 1, NST = 8, BP = NST * 32;
+  static constexpr int XW = (BP + 2 * HP + 2 + 31) / 32 * 32;  // staged x rows (whole 32-row chunk groups)
+  static constexpr int xbytes = XW * 128, bufb = xbytes + BP * 128;
+  static constexpr int kXP = XW / 32, kDP = BP / 32, kCH = kXP + kDP;
+  static constexpr int kLS = 3, kPS = (kCH + kLS - 1) / kLS;  // chunks loaded per step in steps 0 .. kLS - 1
+  static constexpr int kDist = NST - 1 - kLS;                 // set s stored at step s + kDist (<= NST - 2)
+  static constexpr size_t lds = 2 * (size_t)bufb;
+};
+
+template <int W, int H>
+__global__ void __launch_bounds__(256) conv3x3_lin_wgrad_kernel(const bf16_t* __restrict__ x,
+                                                               const bf16_t* __restrict__ dy,
+                                                               float* __restrict__ ws, int N, int C, int K, int G) {
+  using LG = LinGeom<W, H>;
+  constexpr int HP = LG::HP, VR = LG::VR, NST = LG::NST, BP = LG::BP, xbytes = LG::xbytes, bufb = LG::bufb;
+  constexpr int kXP = LG::kXP, kCH = LG::kCH, kPS = LG::kPS, kLS = LG::kLS, kDist = LG::kDist;
+  static_assert(HP % 8 == 0 && kLS + kDist == NST - 1 && kLS * kPS >= kCH, "staging schedule");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, q = (lane & 15) >> 2, pl = lane & 3;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // (band range, channel-block pair) of this workgroup: grid = G * P = 256, XCD = blockIdx % 8
+  const int P = (K >> 6) * (C >> 6), bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+  int rg, pair;
+  if (P <= 32) {
+    rg = xcd * (32 / P) + slot / P;
+    pair = slot % P;
+  } else {
+    const int xr = P >> 5;
+    rg = xcd / xr;
+    pair = (xcd % xr) * 32 + slot;
+  }
+  const int cbn = C >> 6, kb = pair / cbn, cb = pair - kb * cbn;
+  const int T = N * VR * HP, NB = (T + BP - 1) / BP;
+  const int b0 = (int)((long long)NB * rg / G), b1 = (int)((long long)NB * (rg + 1) / G);
+  // buffer descriptors over the whole tensors: an offset past the end reads 0 (the pad and out-of-batch chunks)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)((long long)N * H * W * C * 2),
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc((void*)dy, 0, (int)((long long)N * H * W * K * 2),
+                                                                       0x00020000);
+  const int j = lane >> 3, ch = lane & 7;
+  const int xlane = (j * C + cb * 64 + ch * 8) * 2, dlane = (j * K + kb * 64 + ch * 8) * 2;  // bytes
+  constexpr int kBad = 0x7ffffff0;
+
+  // chunk ci of a band: rows 8 wave + j + 32 ci (x window for ci < kXP, else the band's dy rows); the 8 positions of
+  // a wave's chunk share one virtual row (HP % 8 == 0), so everything but the column is wave-uniform
+  auto cload = [&](int band, int ci) {
+    const bool isx = ci < kXP;
+    const int pos = band * BP + 8 * wave + 32 * (isx ? ci : ci - kXP);  // uniform
+    const int R = pos / HP, cu = pos - R * HP, img = R / VR, rr = R - img * VR;
+    int voff;
+    if (isx) {  // x(img, rr - 1, cu + j - 1)
+      const int lim = (rr >= 1 && img < N) ? W : 0;
+      const int ubase = ((img * H + rr - 1) * W + cu - 1) * C * 2;
+      voff = (unsigned)(cu + j - 1) < (unsigned)lim ? ubase + xlane : kBad;
+    } else {    // dy(img, rr, cu + j)
+      const int lim = (rr < H && img < N) ? W : 0;
+      const int ubase = ((img * H + rr) * W + cu) * K * 2;
+      voff = (unsigned)(cu + j) < (unsigned)lim ? ubase + dlane : kBad;
+    }
+    return __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(isx ? rx : rd, voff, 0, 0));
+  };
+  auto cstore = [&](lds_char* b, int ci, const u32x4v& v) {
+    const int row = 8 * wave + j + 32 * (ci < kXP ? ci : ci - kXP);
+    *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(b + (ci < kXP ? 0 : xbytes) + wswz(row, ch)) = v;
+  };
+
+  // read-address tables (see above): A = dy rows 32 st + 8 g + 4 h + q; B = x rows of the same positions + tap offset
+  auto sw16 = [](int v) { return (v & 7) ^ ((v >> 1) & 4); };
+  // (absolute LDS byte addresses in buffer 0; buffer 1 is bufb higher -- toggled once per band, so every read in
+  // the unrolled steps is table entry + st * 4096, an immediate offset of the ds_read)
+  uint32_t offA[2][4], offB[2][9];
+  const uint32_t base0 = (uint32_t)(uintptr_t)smem;
+  const int sub = (pl & 1) * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 8 * g + 4 * h + q, c8 = (i * 16 + 4 * pl) >> 3;
+      offA[h][i] = base0 + xbytes + r * 128 + ((c8 ^ sw16(r)) << 4) + sub;
+    }
+#pragma unroll
+    for (int jx = 0; jx < 9; ++jx) {
+      const int jj = 9 * wave + jx, t = jj >> 2, dr = t / 3, ds = t - dr * 3, c8 = ((jj & 3) * 16 + 4 * pl) >> 3;
+      const int v = 8 * g + 4 * h + q + dr * HP + ds;
+      offB[h][jx] = base0 + v * 128 + ((c8 ^ sw16(v)) << 4) + sub;
+    }
+  }
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jx = 0; jx < 9; ++jx) acc[i][jx] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (b0 < b1) {
+#pragma unroll
+    for (int ci = 0; ci < kCH; ++ci) cstore(smem, ci, cload(b0, ci));
+  }
+  __syncthreads();
+  u32x4v stg[kLS][kPS];
+  int cur = 0;
+  v8bf a[2][4], b[2][9];
+  auto ldf = [&](int st, v8bf (&af)[4], v8bf (&bf)[9]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)offA[0][i] + st * 512);
+      const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)offA[1][i] + st * 512);
+      af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+#pragma unroll
+    for (int jx = 0; jx < 9; ++jx) {
+      const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)offB[0][jx] + st * 512);
+      const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(uintptr_t)offB[1][jx] + st * 512);
+      bf[jx] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  };
+  ldf(0, a[0], b[0]);
+  for (int band = b0; band < b1; ++band) {
+    const int nb = band + 1 < b1 ? band + 1 : band;  // the last band reloads itself into the unused buffer (no branch)
+    lds_char* other = smem + (cur ^ 1) * bufb;
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      if (st == NST - 1) {
+        // the barrier ending step NST - 2 made the other buffer (stored in steps kDist .. NST - 2) visible and every
+        // read of this one is done: the read tables move over, and the next band's first fragments are read under
+        // this band's last MFMAs (no per-band pipeline drain)
+        const uint32_t delta = cur ? (uint32_t)(-bufb) : (uint32_t)bufb;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) offA[h][i] += delta;
+#pragma unroll
+          for (int jx = 0; jx < 9; ++jx) offB[h][jx] += delta;
+        }
+      }
+      // one scheduling region per step: the next step's 26 fragment reads interleaved one per MFMA with this step's
+      // 36 MFMAs (left alone, the scheduler sinks each read next to its consumer and every 4 MFMAs wait out an LDS
+      // latency; issued as one block, the 4-bit lgkm counter stalls the wave after 15 of them)
+      __builtin_amdgcn_sched_barrier(0);
+      if (st < kLS) {
+#pragma unroll
+        for (int k = 0; k < kPS; ++k)
+          if (st * kPS + k < kCH) stg[st][k] = cload(nb, st * kPS + k);
+      }
+      ldf((st + 1) % NST, a[(st + 1) & 1], b[(st + 1) & 1]);
+#pragma unroll
+      for (int jx = 0; jx < 9; ++jx)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][jx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st & 1][i], b[st & 1][jx], acc[i][jx], 0, 0, 0);
+      if (st >= kDist && st - kDist < kLS) {
+#pragma unroll
+        for (int k = 0; k < kPS; ++k)
+          if ((st - kDist) * kPS + k < kCH) cstore(other, (st - kDist) * kPS + k, stg[st - kDist][k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 26; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st == NST - 2) __syncthreads();  // other buffer complete; this one's last fragments (step NST - 1) read
+    }
+    cur ^= 1;
+  }
+  // this workgroup's 64 x 576 block of slab rg: rows kb * 64 + ..., columns t * C + cb * 64 + ...
+  const int NC = 9 * C;
+  float* slab = ws + (long long)rg * K * NC + (long long)(kb * 64) * NC + cb * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jx = 0; jx < 9; ++jx) {
+      const int jj = 9 * wave + jx, t = jj >> 2, c16 = jj & 3;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slab[(long long)(i * 16 + g * 4 + r) * NC + t * C + c16 * 16 + (lane & 15)] = acc[i][jx][r];
+    }
+}
+
 }  // namespace
 
 static size_t halo_bn_lds(int W) {
@@ -520,6 +722,57 @@ int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, in
   }
   const int total = N * (H / kTH);
   return total < n_cu ? total : n_cu;
+}
+
+// ---- linear-halo weight gradient (3x3 / s1 / p1, C and K multiples of 64, H = W in {7, 14, 28}) ----
+static int g_lin_wgrad = 1;
+void conv3x3_lin_wgrad_set(int on) { g_lin_wgrad = on; }  // 0 off (implicit GEMM), 1 on
+
+static constexpr int kLinGrid = 256;
+static int lin_pairs(int C, int K) { return (C / 64) * (K / 64); }
+
+int conv3x3_lin_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
+  if (!g_lin_wgrad || R != 3 || S != 3 || stride != 1 || pad != 1 || (stride_w != 0 && stride_w != 1) || H != W ||
+      (W != 7 && W != 14 && W != 28) || C % 64 || K % 64)
+    return 0;
+  const int P = lin_pairs(C, K);
+  // grid = 256 workgroups = (band ranges) x (channel-block pairs); pairs of one range on one XCD (or two)
+  if (!(P == 1 || P == 2 || P == 4 || P == 8 || P == 16 || P == 32 || P == 64 || P == 128 || P == 256)) return 0;
+  // 32-bit positions and byte offsets (buffer loads)
+  if ((long long)N * (H + 1) * ((W + 8) / 8 * 8) >= (1LL << 30) || 2LL * N * H * W * (C > K ? C : K) >= (1LL << 31))
+    return 0;
+  static bool init = false;
+  if (!init) {
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_lin_wgrad_kernel<28, 28>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_lin_wgrad_kernel<14, 14>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)conv3x3_lin_wgrad_kernel<7, 7>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    init = true;
+  }
+  return kLinGrid / P;  // split-K slabs = band ranges
+}
+
+void conv3x3_lin_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int split, int N, int H, int W, int C, int K,
+                       hipStream_t st) {
+  const int P = lin_pairs(C, K);
+  if (split * P != kLinGrid)
+    throw std::runtime_error("conv3x3_lin_wgrad: split x channel-block pairs != 256 workgroups");
+  const dim3 grid(kLinGrid);
+  const size_t lds28 = LinGeom<28, 28>::lds, lds14 = LinGeom<14, 14>::lds, lds7 = LinGeom<7, 7>::lds;
+  if (W == 28)
+    hipLaunchKernelGGL((conv3x3_lin_wgrad_kernel<28, 28>), grid, dim3(256), lds28, st, x, dy, ws,
+                       N, C, K, split);
+  else if (W == 14)
+    hipLaunchKernelGGL((conv3x3_lin_wgrad_kernel<14, 14>), grid, dim3(256), lds14, st, x, dy, ws,
+                       N, C, K, split);
+  else if (W == 7)
+    hipLaunchKernelGGL((conv3x3_lin_wgrad_kernel<7, 7>), grid, dim3(256), lds7, st, x, dy, ws,
+                       N, C, K, split);
+  else
+    throw std::runtime_error("conv3x3_lin_wgrad: no instance for this width");
+  DTG_LAUNCH_CHECK();
 }
 
 void conv3x3_halo_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int grid, int N, int H, hipStream_t st) {

@@ -200,3 +200,32 @@ def test_conv_wgrad_halo_64(N, beta, bf16_out):
         assert _rel(dw, ref) < (1e-2 if bf16_out else 2e-3)
         outs.append(dw.float())
     assert _rel(outs[0], outs[1]) < (1e-2 if bf16_out else 2e-3)
+
+
+@pytest.mark.parametrize("N,H,C,K,beta", [(40, 28, 128, 128, 0.0), (64, 14, 256, 256, 1.0), (64, 7, 512, 512, 0.0),
+                                          (12, 28, 64, 128, 0.0), (20, 14, 256, 128, 0.0), (9, 7, 128, 512, 1.0)])
+def test_conv_wgrad_lin_halo(N, H, C, K, beta):
+    """conv_wgrad for the 3x3 / s1 / p1 layers of ResNet stages 2-4 (28x28 x 128, 14x14 x 256, 7x7 x 512) runs the
+    linear-halo weight gradient (csrc/kernels/conv_halo.hip conv3x3_lin_wgrad_kernel: the batch as one tall image
+    with shared zero rows / columns, 64 x 576 blocks per workgroup, XCD-grouped channel-block pairs): against the fp32
+    conv2d_weight and the implicit-GEMM wgrad (conv_lin_wgrad_set(0)).  The first three shapes put 2-4 bands on
+    every persistent workgroup (the pipelined next-band staging); the others cover C != K block pairs."""
+    from dtg.ops._native import lib
+    L = lib()
+    g = torch.Generator(device="cpu").manual_seed(70 + N + H + C + K)
+    x = torch.randn(N, H, H, C, generator=g).to(DEV, torch.bfloat16)
+    dy = torch.randn(N, H, H, K, generator=g).to(DEV, torch.bfloat16)
+    dw0 = torch.randn(K, 3, 3, C, generator=g).to(DEV)
+    ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, 3, 3), dy.float().permute(0, 3, 1, 2),
+                                      padding=1).permute(0, 2, 3, 1) + beta * dw0
+    outs = []
+    for on in (1, 0):
+        dw = dw0.clone()
+        L.conv_lin_wgrad_set(on)
+        try:
+            L.conv_wgrad(dy, x, dw, beta, 1, 1)
+        finally:
+            L.conv_lin_wgrad_set(1)
+        assert _rel(dw, ref) < 2e-3, (on, _rel(dw, ref))
+        outs.append(dw)
+    assert _rel(outs[0], outs[1]) < 2e-3

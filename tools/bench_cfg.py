@@ -9,6 +9,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
     DTG_AB_HALO=0 python tools/bench_cfg.py           # the implicit-GEMM stage-1 3x3 forward instead of the halo one
     DTG_AB_HALO_DGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 dgrad instead of the halo one
     DTG_AB_HALO_WGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 wgrad instead of the halo one
+    DTG_AB_LIN_WGRAD=0 python tools/bench_cfg.py      # the implicit-GEMM stage-2..4 3x3 wgrads instead of the linear halo
 """
 import os
 import runpy
@@ -28,6 +29,8 @@ if os.environ.get("DTG_AB_HALO_DGRAD"):  # 0: the implicit-GEMM dgrad for the st
     lib().conv_halo_dgrad_set(int(os.environ["DTG_AB_HALO_DGRAD"]))
 if os.environ.get("DTG_AB_HALO_WGRAD"):  # 0: the implicit-GEMM wgrad for the stage-1 3x3 (conv_halo.hip)
     lib().conv_halo_wgrad_set(int(os.environ["DTG_AB_HALO_WGRAD"]))
+if os.environ.get("DTG_AB_LIN_WGRAD"):  # 0: the implicit-GEMM wgrad for the stage-2..4 3x3s (conv_halo.hip lin)
+    lib().conv_lin_wgrad_set(int(os.environ["DTG_AB_LIN_WGRAD"]))
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
