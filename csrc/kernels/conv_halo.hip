@@ -482,16 +482,17 @@ __global__ void __launch_bounds__(256) conv3x3_lin_wgrad_kernel(const bf16_t* __
   lds_char* smem = (lds_char*)smem_raw;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, q = (lane & 15) >> 2, pl = lane & 3;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // (band range, channel-block pair) of this workgroup: grid = G * P = 256, XCD = blockIdx % 8
-  const int P = (K >> 6) * (C >> 6), bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
+  // (band range, channel-block pair) of this workgroup: grid = G * P (a power of 2 >= 8), XCD = blockIdx % 8, so
+  // an XCD holds gridDim / 8 slots; the pairs of one band range fill an XCD's slots (or span P / slots XCDs)
+  const int P = (K >> 6) * (C >> 6), bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3, slots = gridDim.x >> 3;
   int rg, pair;
-  if (P <= 32) {
-    rg = xcd * (32 / P) + slot / P;
+  if (P <= slots) {
+    rg = xcd * (slots / P) + slot / P;
     pair = slot % P;
   } else {
-    const int xr = P >> 5;
+    const int xr = P / slots;
     rg = xcd / xr;
-    pair = (xcd % xr) * 32 + slot;
+    pair = (xcd % xr) * slots + slot;
   }
   const int cbn = C >> 6, kb = pair / cbn, cb = pair - kb * cbn;
   const int T = N * VR * HP, NB = (T + BP - 1) / BP;
@@ -704,7 +705,9 @@ static size_t halo_wgrad_lds() {
   return 2 * (size_t)(halo + dyb);
 }
 static int g_halo_wgrad = 1;
-void conv3x3_halo_wgrad_set(int on) { g_halo_wgrad = on; }  // 0 off, 1 on (2 / 3: shorter staging distance)
+// 0 off, 1 on (2 / 3: shorter staging distance), >= 8: on with at most that many workgroups (A/B runs: a side-stream
+// grid below the CU count leaves CUs to the main stream)
+void conv3x3_halo_wgrad_set(int on) { g_halo_wgrad = on; }
 
 int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
   if (!g_halo_wgrad || C != kC || K != kC || R != 3 || S != 3 || stride != 1 || pad != 1 ||
@@ -720,15 +723,22 @@ int conv3x3_halo_wgrad_split(int N, int H, int W, int C, int K, int R, int S, in
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     n_cu = halo_cus();
   }
-  const int total = N * (H / kTH);
-  return total < n_cu ? total : n_cu;
+  const int total = N * (H / kTH), cap = g_halo_wgrad >= 8 && g_halo_wgrad < n_cu ? g_halo_wgrad : n_cu;
+  return total < cap ? total : cap;
 }
 
 // ---- linear-halo weight gradient (3x3 / s1 / p1, C and K multiples of 64, H = W in {7, 14, 28}) ----
+// 0 off (implicit GEMM), 1 on (128 workgroups), a power of 2 in [64, 256]: on with that many workgroups.  The kernel
+// runs on the weight-gradient side stream, one 155-KB-LDS workgroup per CU, so its grid is the number of CUs the main
+// stream's kernels cannot use while it runs: 128 workgroups measured +0.5 % on the ResNet step against 256 (in 2.1x
+// the kernel time) and 64 -0.3 % against 128 (profiles/r06_lin_wgrad/ab_grid*.log)
+static constexpr int kLinGridDefault = 128;
 static int g_lin_wgrad = 1;
-void conv3x3_lin_wgrad_set(int on) { g_lin_wgrad = on; }  // 0 off (implicit GEMM), 1 on
-
-static constexpr int kLinGrid = 256;
+static int g_lin_grid = kLinGridDefault;
+void conv3x3_lin_wgrad_set(int on) {
+  g_lin_wgrad = on;
+  g_lin_grid = (on >= 64 && on <= 256 && (on & (on - 1)) == 0) ? on : kLinGridDefault;
+}
 static int lin_pairs(int C, int K) { return (C / 64) * (K / 64); }
 
 int conv3x3_lin_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int stride_w) {
@@ -737,7 +747,9 @@ int conv3x3_lin_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int
     return 0;
   const int P = lin_pairs(C, K);
   // grid = 256 workgroups = (band ranges) x (channel-block pairs); pairs of one range on one XCD (or two)
-  if (!(P == 1 || P == 2 || P == 4 || P == 8 || P == 16 || P == 32 || P == 64 || P == 128 || P == 256)) return 0;
+  // P and the per-XCD slot count must divide one another, and a range may span at most the 8 XCDs
+  const int slots = g_lin_grid / 8;
+  if ((P & (P - 1)) != 0 || P > g_lin_grid || (P > slots && P / slots > 8)) return 0;
   // 32-bit positions and byte offsets (buffer loads)
   if ((long long)N * (H + 1) * ((W + 8) / 8 * 8) >= (1LL << 30) || 2LL * N * H * W * (C > K ? C : K) >= (1LL << 31))
     return 0;
@@ -751,15 +763,16 @@ int conv3x3_lin_wgrad_split(int N, int H, int W, int C, int K, int R, int S, int
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     init = true;
   }
-  return kLinGrid / P;  // split-K slabs = band ranges
+  return g_lin_grid / P;  // split-K slabs = band ranges
 }
 
 void conv3x3_lin_wgrad(const bf16_t* dy, const bf16_t* x, float* ws, int split, int N, int H, int W, int C, int K,
                        hipStream_t st) {
   const int P = lin_pairs(C, K);
-  if (split * P != kLinGrid)
-    throw std::runtime_error("conv3x3_lin_wgrad: split x channel-block pairs != 256 workgroups");
-  const dim3 grid(kLinGrid);
+  const int wgs = split * P;
+  if (wgs < 8 || (wgs & (wgs - 1)) != 0)
+    throw std::runtime_error("conv3x3_lin_wgrad: split x channel-block pairs must be a power of 2 >= 8");
+  const dim3 grid(wgs);
   const size_t lds28 = LinGeom<28, 28>::lds, lds14 = LinGeom<14, 14>::lds, lds7 = LinGeom<7, 7>::lds;
   if (W == 28)
     hipLaunchKernelGGL((conv3x3_lin_wgrad_kernel<28, 28>), grid, dim3(256), lds28, st, x, dy, ws,

@@ -219,7 +219,7 @@ def test_conv_wgrad_lin_halo(N, H, C, K, beta):
     ref = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (K, C, 3, 3), dy.float().permute(0, 3, 1, 2),
                                       padding=1).permute(0, 2, 3, 1) + beta * dw0
     outs = []
-    for on in (1, 0):
+    for on in (1, 256, 0):  # 128 workgroups (default), 256 (conv_lin_wgrad_set(256): other XCD slot mapping), implicit
         dw = dw0.clone()
         L.conv_lin_wgrad_set(on)
         try:
@@ -228,4 +228,4 @@ def test_conv_wgrad_lin_halo(N, H, C, K, beta):
             L.conv_lin_wgrad_set(1)
         assert _rel(dw, ref) < 2e-3, (on, _rel(dw, ref))
         outs.append(dw)
-    assert _rel(outs[0], outs[1]) < 2e-3
+    assert _rel(outs[0], outs[2]) < 2e-3 and _rel(outs[1], outs[2]) < 2e-3

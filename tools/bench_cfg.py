@@ -10,6 +10,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
     DTG_AB_HALO_DGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 dgrad instead of the halo one
     DTG_AB_HALO_WGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 wgrad instead of the halo one
     DTG_AB_LIN_WGRAD=0 python tools/bench_cfg.py      # the implicit-GEMM stage-2..4 3x3 wgrads instead of the linear halo
+    DTG_AB_LIN_WGRAD=256 python tools/bench_cfg.py    # the linear-halo wgrads on 256 workgroups (halo: DTG_AB_HALO_WGRAD=128)
 """
 import os
 import runpy
