@@ -168,39 +168,6 @@ std::vector<Tensor> stem_bn_pool_bwd(Tensor dout, Tensor idx, Tensor y, Tensor g
   return {dy, dgamma, dbeta};
 }
 
-// stem_bn_pool_bwd with the pixel-pair conv's weight gradient fused into pass 2: dy never materialises.  x8 the pair
-// input [N, Hp, Wq, 8], dwp [K, 7, 4, 8] fp32 (overwritten).  Returns false when the geometry is not covered (nothing
-// written; the caller runs stem_bn_pool_bwd + conv_wgrad).
-bool stem_bn_pool_bwd_wgrad(Tensor dout, Tensor idx, Tensor y, Tensor gamma, Tensor beta, Tensor smean, Tensor sinv,
-                            int64_t k, int64_t s, int64_t pad, Tensor x8, Tensor dwp, Tensor dgamma_acc,
-                            Tensor dbeta_acc, Tensor yam) {
-  check_nhwc8(dout, "dout");
-  check_nhwc8(y, "y");
-  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kByte && idx.sizes() == dout.sizes() && idx.is_contiguous(),
-              "idx must be uint8 shaped like dout");
-  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
-  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
-  TORCH_CHECK(dout.size(0) == N && dout.size(1) == P && dout.size(2) == Q && dout.size(3) == C,
-              "dout shape does not match the pooled geometry of y");
-  TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kBFloat16 && x8.dim() == 4 && x8.is_contiguous() &&
-                  x8.size(0) == N && x8.size(3) == 8, "x8 must be the [N, Hp, Wq, 8] pixel-pair input");
-  TORCH_CHECK(dwp.is_cuda() && dwp.scalar_type() == at::kFloat && dwp.is_contiguous() && dwp.numel() == C * 224 &&
-                  dwp.size(0) == C, "dwp must be a contiguous fp32 [K, 7, 4, 8]");
-  TORCH_CHECK(yam.is_cuda() && yam.scalar_type() == at::kBFloat16 && yam.sizes() == dout.sizes() && yam.is_contiguous(),
-              "yam must be the forward's bf16 y-at-argmax tensor");
-  for (auto* t : {&gamma, &beta, &smean, &sinv, &dgamma_acc, &dbeta_acc}) check_chan(*t, C, "per-channel tensor");
-  TORCH_CHECK(y.numel() / 8 < (1LL << 31), "stem kernels index 16-byte vectors with 32-bit math");
-  const int Hp = x8.size(1), Wq = x8.size(2);
-  if (!dtg::stem_bwd_wgrad_ok(H, W, C, (int)k, (int)s, (int)pad, P, Q, Hp, Wq)) return false;
-  c10::DeviceGuard dg(y.device());
-  auto ws = at::empty({dtg::stem_bwd_wgrad_ws_floats((long long)N * H * W, C)}, y.options().dtype(at::kFloat));
-  return dtg::stem_bn_pool_bwd_wgrad(cbfp(dout), idx.data_ptr<uint8_t>(), cbfp(y), gamma.data_ptr<float>(),
-                                     beta.data_ptr<float>(), smean.data_ptr<float>(), sinv.data_ptr<float>(), cbfp(x8),
-                                     Hp, Wq, dwp.data_ptr<float>(), dgamma_acc.data_ptr<float>(),
-                                     dbeta_acc.data_ptr<float>(), 1, ws.data_ptr<float>(), N, H, W, C, (int)k, (int)s,
-                                     (int)pad, P, Q, cur_stream(), cbfp(yam));
-}
-
 // x [N,H,W,C] (any C) -> cols [N*P*Q, Kp] bf16, Kp >= R*S*C, multiple of 8
 Tensor im2col(Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t Kp) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(), "x NHWC bf16");
@@ -244,7 +211,6 @@ void register_pool_ops(pybind11::module_& m) {
         pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("smean"), pybind11::arg("sinv"),
         pybind11::arg("k"), pybind11::arg("s"), pybind11::arg("pad"), pybind11::arg("dgamma_acc") = pybind11::none(),
         pybind11::arg("dbeta_acc") = pybind11::none(), pybind11::arg("yam") = pybind11::none());
-  m.def("stem_bn_pool_bwd_wgrad", &stem_bn_pool_bwd_wgrad);
   m.def("im2col", &im2col);
   m.def("col2im", &col2im);
 }

@@ -242,14 +242,6 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
                       const float* smean, const float* sinv, bf16_t* dy, float* dgamma, float* dbeta, int accum,
                       float* ws, int N, int H, int W, int C, int k, int s, int pad, int P, int Q, hipStream_t st,
                       const bf16_t* yam = nullptr);
-// stem backward pass 2 fused with the pixel-pair conv's weight gradient (stem.hip stem_bwd_wgrad_kernel): dwp
-// [K][7][4][8] fp32 overwritten; false (nothing launched) when the geometry is not covered
-bool stem_bwd_wgrad_ok(int H, int W, int C, int k, int s, int pad, int P, int Q, int Hp, int Wq);
-long long stem_bwd_wgrad_ws_floats(long long M, int C);
-bool stem_bn_pool_bwd_wgrad(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma,
-                            const float* beta, const float* smean, const float* sinv, const bf16_t* x8, int Hp, int Wq,
-                            float* dwp, float* dgamma, float* dbeta, int accum, float* ws, int N, int H, int W, int C,
-                            int k, int s, int pad, int P, int Q, hipStream_t st, const bf16_t* yam);
 
 // ---- im2col / col2im, NHWC (im2col.hip) --------------------------------------------------------
 void im2col(const bf16_t* x, bf16_t* cols, int N, int H, int W, int C, int R, int S, int stride, int pad, int Kp,

@@ -23,7 +23,6 @@
 #include "dtg/kernels.h"
 #include "dtg/bn_finalize.cuh"
 #include "dtg/mfma_gemm.cuh"  // gemm::FastDiv
-#include "dtg/gemm_epi.cuh"   // Epi, gemm_splitk_reduce
 
 namespace dtg {
 
@@ -486,247 +485,6 @@ __global__ void __launch_bounds__(256) stem_bwd_band_kernel(const bf16_t* __rest
   }
 }
 
-// ---- backward pass 2 fused with the stem conv's weight gradient (pixel-pair form) ----------------------------------
-// Pass 2 writes dy = a*dp + bx*y + c0 ([N, 112, 112, 64], 1.64 GB at b1024) for the conv's weight gradient alone,
-// which reads it straight back (conv_wgrad over the pixel-pair input).  Here the same dy values are computed into
-// LDS, two conv-output rows (224 pixels) at a time, and reduced at once into dW = dy^T X with MFMAs, X being the
-// pixel-pair im2col of the staged input rows -- dy never reaches HBM (3.3 GB less traffic per step).
-// Geometry (ResNet stem, the pair form of ops/conv.py stem_pairs): conv output H x W = 112 x 112, 64 channels; x8
-// [N, Hp, Wq, 8] with Hp >= 2 H + 5, Wq >= W + 3; taps r < 7 (row stride 2), s < 4 (pair column stride 1); dW is
-// [64][7][4][8] = 64 x 224.  A workgroup (2 per CU, persistent) walks a contiguous run of 2-row bands:
-//   stage the 2 pooled rows (dout + argmax) and the 9 x8 rows the band reaches, and load y for its 224 x 64 values;
-//   dy -> LDS [224 pixels][64] (the transposed-read swizzle of the halo kernels);
-//   7 steps of 32 pixels: A = dy^T fragments (ds_read_b64_tr_b16), B = X fragments gathered from the x8 rows
-//   (each lane's 4-pixel group reads one tap's 4 channels of 4 consecutive pixel pairs), 16x16x32 MFMAs into a
-//   64 x 64 (waves 0, 1) or 64 x 48 (waves 2, 3) register block of the 64 x 224 partial.
-// One fp32 slab per workgroup, summed by the split-K reduce.
-typedef unsigned int sf_u32x2 __attribute__((ext_vector_type(2)));
-using gemm::lds_char;
-using gemm::lds_v4bf;
-using gemm::sel;
-using gemm::v4bf;
-using gemm::v8bf;
-constexpr int kSfBand = 2, kSfR = 7, kSfS = 4, kSfCols = kSfR * kSfS * 8;  // 224
-constexpr int kSfXRows = 2 * kSfBand + kSfR - 2;                           // 9 x8 rows per band
-__device__ __forceinline__ int sf_swz(int row, int chunk) {  // 128-B rows, as conv_halo.hip wswz
-  return row * 128 + ((chunk ^ (row & 7) ^ ((row >> 1) & 4)) << 4);
-}
-
-struct StemFusedArgs {
-  const bf16_t* dout;
-  const uint8_t* idx;
-  const bf16_t* y;
-  const bf16_t* x8;
-  const float* gamma;
-  const float* beta;
-  const float* smean;
-  const float* sinv;
-  const float* coef;
-  float* ws;
-  int Wq;  // x8 pair columns
-  int Hp;  // x8 rows
-};
-
-__global__ void __launch_bounds__(256, 2) stem_bwd_wgrad_kernel(StemFusedArgs A, StemGeom g) {
-  constexpr int C = 64;
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  lds_char* lds = (lds_char*)lds_raw;
-  const int W = g.W, Q = g.Q, Wq = A.Wq;
-  const int npx = kSfBand * W;                       // 224 pixels per band
-  lds_char* dyt = lds;                               // [npx][64] bf16, swizzled rows
-  auto kb = [](int b) { return (b + 1023) / 1024 * 1024; };  // regions in whole 1-KB DMA pieces
-  lds_char* sd = dyt + npx * 128;                    // [2][Q][64] bf16 pooled gradient
-  lds_char* si = sd + kb(2 * Q * C * 2);             // [2][Q][64] u8 argmax
-  lds_char* xs = si + kb(2 * Q * C);                 // [9][Wq][8] bf16 input rows
-  const int tid = threadIdx.x, lane = tid & 63, g16 = lane >> 4, q = (lane & 15) >> 2, pl = lane & 3;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bands = g.H / kSfBand, total = g.N * bands;
-  const int b0 = (int)((long long)blockIdx.x * total / gridDim.x);
-  const int b1 = (int)((long long)(blockIdx.x + 1) * total / gridDim.x);
-
-  const int c8 = tid & 7, c0 = c8 * 8;  // this thread's 8 channels of the dy computation (fixed)
-  float sc[8], sf[8], ca[8], cbx[8], cc[8];
-  {
-    float mu[8], is[8], ga[8], be[8];
-    load8_f32(A.smean + c0, mu);
-    load8_f32(A.sinv + c0, is);
-    load8_f32(A.gamma + c0, ga);
-    load8_f32(A.beta + c0, be);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      sc[k] = ga[k] * is[k];
-      sf[k] = be[k] - mu[k] * sc[k];
-    }
-    load8_f32(A.coef + c0, ca);
-    load8_f32(A.coef + C + c0, cbx);
-    load8_f32(A.coef + 2 * C + c0, cc);
-  }
-  // MFMA work split: 14 column tiles of 16 (two taps each) -> waves 0, 1: 4 tiles, waves 2, 3: 3 tiles
-  const int jt0 = wave < 2 ? 4 * wave : 8 + 3 * (wave - 2), njt = wave < 2 ? 4 : 3;
-  // per-lane constants: A reads (dy rows 8 g + 4 h + q of a step), B reads (tap of column group pl, 8-byte half)
-  int offA[2][4];
-  auto sw16 = [](int v) { return (v & 7) ^ ((v >> 1) & 4); };
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = 8 * g16 + 4 * h + q, ch = (i * 16 + 4 * pl) >> 3;
-      offA[h][i] = r * 128 + ((ch ^ sw16(r)) << 4) + (pl & 1) * 8;
-    }
-  int tapoff[4];  // byte offset of tap t = 2 (jt0 + j) + pl / 2 in the staged x8 rows, + the 8-byte half
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int t = 2 * (jt0 + (j < njt ? j : 0)) + (pl >> 1), r = t / kSfS, s = t - r * kSfS;
-    tapoff[j] = (r * Wq + s) * 16 + (pl & 1) * 8;
-  }
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  constexpr int kYU = 7;  // y chunks per thread per band: at most 224 pixels x 8 chunks / 256 (W <= 112)
-  const int njobs = npx * 8;
-  for (int band = b0; band < b1; ++band) {
-    const int n = band / bands, h0 = (band - n * bands) * kSfBand, p0 = h0 >> 1;
-    // y for this band's dy values: issued first, consumed after the staging
-    uint4 yv[kYU];
-#pragma unroll
-    for (int u = 0; u < kYU; ++u) {
-      if (tid + 256 * u < njobs) {
-        const int pix = (tid + 256 * u) >> 3, hr = pix / W, w = pix - hr * W;
-        yv[u] = *reinterpret_cast<const uint4*>(A.y + (((long long)n * g.H + h0 + hr) * W + w) * C + c0);
-      }
-    }
-    __syncthreads();  // the previous band's MFMA reads of dyt / xs are done
-    // staging by LDS-DMA (global_load_lds, 16 B per lane, 1 KB per wave-instruction): the pooled rows p0, p0 + 1
-    // (gradient, then argmax) and the x8 rows 2 h0 .. 2 h0 + 8 are contiguous in global memory and in LDS, so all
-    // of a band's staging is in flight at once with the y loads above -- one memory latency per band.  Pieces past
-    // a region's end (or a pooled row past P) read the zero page.
-    {
-      const long long pool0 = ((long long)n * g.P + p0) * Q * C;          // elements
-      const long long pool_end = (long long)g.N * g.P * Q * C;
-      const int sdb = 2 * Q * C * 2, sib = 2 * Q * C, xsb = kSfXRows * Wq * 16;  // bytes
-      const bf16_t* x8r = A.x8 + (((long long)n * A.Hp + 2 * h0) * Wq) * 8;
-      const int npieces = (sdb + 1023) / 1024 + (sib + 1023) / 1024 + (xsb + 1023) / 1024;
-      for (int pc = wave; pc < npieces; pc += 4) {
-        const int psd = (sdb + 1023) / 1024, psi = (sib + 1023) / 1024;
-        const char* src;
-        lds_char* dst;
-        if (pc < psd) {
-          const int off = pc * 1024 + lane * 16;
-          const bool ok = off < sdb && pool0 + off / 2 < pool_end;
-          src = (const char*)sel(ok, (const char*)(A.dout + pool0) + off);
-          dst = sd + pc * 1024;
-        } else if (pc < psd + psi) {
-          const int off = (pc - psd) * 1024 + lane * 16;
-          const bool ok = off < sib && pool0 + off < pool_end;
-          src = (const char*)sel(ok, (const char*)(A.idx + pool0) + off);
-          dst = si + (pc - psd) * 1024;
-        } else {
-          const int off = (pc - psd - psi) * 1024 + lane * 16;
-          src = (const char*)sel(off < xsb, (const char*)x8r + off);
-          dst = xs + (pc - psd - psi) * 1024;
-        }
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-      }
-    }
-    __syncthreads();
-    // dy = a*dp + bx*y + c0 (pass 2 of stem_bwd_band_kernel, same terms) -> dyt
-#pragma unroll
-    for (int u = 0; u < kYU; ++u) {
-      if (tid + 256 * u >= njobs) continue;
-      const int pix = (tid + 256 * u) >> 3, hr = pix / W, w = pix - hr * W, h = h0 + hr;
-      float yf[8];
-      {
-        const uint32_t d[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          yf[2 * k] = __uint_as_float(d[k] << 16);
-          yf[2 * k + 1] = __uint_as_float(d[k] & 0xffff0000u);
-        }
-      }
-      const int hp = h + 1, wp = w + 1;  // padded coordinates
-      const int p_hi = min(g.P - 1, hp >> 1), q_hi = min(Q - 1, wp >> 1);
-      const int p_lo = hp >= 3 ? ((hp - 3) >> 1) + 1 : 0, q_lo = wp >= 3 ? ((wp - 3) >> 1) + 1 : 0;
-      float accd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int p = p_hi - 1 + (j >> 1), qq = q_hi - 1 + (j & 1);
-        if (p >= p_lo && qq >= q_lo) {
-          const int li = ((p - p0) * Q + qq) * C + c0;
-          const u32x4v dv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4v*>(sd + li * 2);
-          const sf_u32x2 pk = *reinterpret_cast<const __attribute__((address_space(3))) sf_u32x2*>(si + li);
-          const uint32_t wi = (uint32_t)((hp - 2 * p) * 3 + (wp - 2 * qq));
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t word = k < 4 ? pk.x : pk.y;
-            const uint32_t pair = (k >> 1) == 0 ? dv.x : (k >> 1) == 1 ? dv.y : (k >> 1) == 2 ? dv.z : dv.w;
-            const float d = __uint_as_float((k & 1) ? (pair & 0xffff0000u) : (pair << 16));
-            accd[k] += ((word >> (8 * (k & 3))) & 0xffu) == wi ? d : 0.f;
-          }
-        }
-      }
-      uint32_t o2[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float o[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int kk = 2 * k + e;
-          const float dp = fmaf(yf[kk], sc[kk], sf[kk]) > 0.f ? accd[kk] : 0.f;
-          o[e] = fmaf(ca[kk], dp, fmaf(cbx[kk], yf[kk], cc[kk]));
-        }
-        o2[k] = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      }
-      *reinterpret_cast<__attribute__((address_space(3))) u32x4v*>(dyt + sf_swz(pix, c8)) =
-          u32x4v{o2[0], o2[1], o2[2], o2[3]};
-    }
-    __syncthreads();
-    // dW += dy^T X over the band's 224 pixels: 7 steps of 32
-#pragma unroll
-    for (int st = 0; st < npx / 32; ++st) {
-      v8bf a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(dyt + st * 4096 + offA[0][i]));
-        const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(dyt + st * 4096 + offA[1][i]));
-        a[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-      int rb[2];  // x8 byte offset of this lane's pixel (row 2 hl, pair column w), pixel 32 st + 8 g + 4 h + q
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int pix = 32 * st + 8 * g16 + 4 * h + q, hl = pix >= W ? 1 : 0, w = pix - hl * W;
-        rb[h] = (2 * hl * Wq + w) * 16;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(xs + rb[0] + tapoff[j]));
-        const v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(xs + rb[1] + tapoff[j]));
-        b[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j < njt) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  }
-  float* slab = A.ws + (long long)blockIdx.x * (C * kSfCols);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < njt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          slab[(i * 16 + g16 * 4 + r) * kSfCols + (jt0 + j) * 16 + (lane & 15)] = acc[i][j][r];
-      }
-}
-
 // dynamic LDS of the banded backward (see stem_bn_pool_bwd); must fit one workgroup's LDS (160 KB on gfx950),
 // larger images (wide rows) take the per-pixel gather form instead
 static size_t stem_band_lds(int Q, int C) {
@@ -871,54 +629,6 @@ void stem_bn_pool_bwd(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, c
   dim3 ga((unsigned)((M + rpa - 1) / rpa), bg.gy);
   DTG_TPR_SWITCH(bg.tpr, stem_bwd_dx_kernel<T><<<ga, kBlk, 0, st>>>(dout, idx, y, gamma, beta, smean, sinv, coef, g, M,
                                                                    rpa, dy)); DTG_LAUNCH_CHECK();
-}
-
-// Stem backward with the conv's weight gradient fused into pass 2 (stem_bwd_wgrad_kernel): pass 1 and the finalize as
-// in stem_bn_pool_bwd, then the fused pass writes one 64 x 224 fp32 slab per workgroup and the split-K reduce sums
-// them into dwp [64][7][4][8].  Returns false (nothing launched) when the geometry is not the ResNet pair form.
-static constexpr int kSfGrid = 512;
-static size_t stem_fused_lds(int W, int Q, int Wq) {  // the staged regions are filled in whole 1-KB DMA pieces
-  auto kb = [](size_t b) { return (b + 1023) / 1024 * 1024; };
-  return (size_t)kSfBand * W * 128 + kb(2 * (size_t)Q * 64 * 2) + kb(2 * (size_t)Q * 64) + kb((size_t)kSfXRows * Wq * 16);
-}
-bool stem_bwd_wgrad_ok(int H, int W, int C, int k, int s, int pad, int P, int Q, int Hp, int Wq) {
-  return C == 64 && k == 3 && s == 2 && pad == 1 && H % kSfBand == 0 && P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 &&
-         (kSfBand * W) % 32 == 0 && kSfBand * W <= 224 && Hp >= 2 * H + 5 && Wq >= W + 3 &&
-         stem_fused_lds(W, Q, Wq) <= 80 * 1024;
-}
-long long stem_bwd_wgrad_ws_floats(long long M, int C) {
-  return stem_bwd_workspace_floats(M, C) + (long long)kSfGrid * C * kSfCols;
-}
-bool stem_bn_pool_bwd_wgrad(const bf16_t* dout, const uint8_t* idx, const bf16_t* y, const float* gamma,
-                            const float* beta, const float* smean, const float* sinv, const bf16_t* x8, int Hp, int Wq,
-                            float* dwp, float* dgamma, float* dbeta, int accum, float* ws, int N, int H, int W, int C,
-                            int k, int s, int pad, int P, int Q, hipStream_t st, const bf16_t* yam) {
-  if (!stem_bwd_wgrad_ok(H, W, C, k, s, pad, P, Q, Hp, Wq) || !yam || !stem_pooled_stats_ok(C)) return false;
-  const long long M = (long long)N * H * W;
-  const BnGeom bg = stem_reduce_geom(M, C);
-  const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
-  float* part = ws;
-  float* coef = ws + stem_part_slots(bg) * 2 * C;
-  float* slabs = ws + stem_bwd_workspace_floats(M, C);
-  fill_zero(part, (long long)kBnStatSlots * 2 * C * sizeof(float), st);
-  const long long chunks = (long long)N * P * Q * (C / 8);
-  hipLaunchKernelGGL(stem_bwd_pooled_stats_kernel<4>, dim3(grid_for(chunks, 256, 2048)), dim3(256), 0, st, dout, yam,
-                     gamma, beta, smean, sinv, C, chunks, part); DTG_LAUNCH_CHECK();
-  bn_finalize_kernel<16><<<(C + 63) / 64, 1024, 0, st>>>(part, kBnStatSlots, M, C, accum ? 2 : 1, gamma, nullptr, nullptr,
-                                                         nullptr, const_cast<float*>(smean), const_cast<float*>(sinv),
-                                                         0.f, 0.f, coef, dgamma, dbeta); DTG_LAUNCH_CHECK();
-  static bool attr = false;
-  if (!attr) {
-    DTG_HIP_CHECK(hipFuncSetAttribute((const void*)stem_bwd_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      80 * 1024));
-    attr = true;
-  }
-  const int total = N * (H / kSfBand), grid = total < kSfGrid ? total : kSfGrid;
-  StemFusedArgs a{dout, idx, y, x8, gamma, beta, smean, sinv, coef, slabs, Wq, Hp};
-  hipLaunchKernelGGL(stem_bwd_wgrad_kernel, dim3(grid), dim3(256), stem_fused_lds(W, Q, Wq), st, a, g);
-  DTG_LAUNCH_CHECK();
-  gemm_splitk_reduce(slabs, grid, C, kSfCols, Epi{dwp, kSfCols, 0, 1.f, 0.f, nullptr, 0}, st);
-  return true;
 }
 
 // Stem weight gradient from the padded-channel wgrad layouts into the parameter's own [K, R, S, C] memory

@@ -382,10 +382,6 @@ _STEM_YAM = True
 # 0 / 0 restore the defaults
 _STEM_WG_SCHED = 3
 _STEM_WG_WGS = 512
-# _STEM_FUSED_WG = True: the backward's pass 2 (dy = a*dp + bx*y + c0) and the stem conv's weight gradient in one
-# kernel (csrc/kernels/stem.hip stem_bwd_wgrad_kernel): dy is reduced from LDS into dW and never written (3.3 GB less
-# HBM traffic per step at b1024); False: stem_bn_pool_bwd + conv_wgrad (A/B tests)
-_STEM_FUSED_WG = False
 
 
 class _StemFn(torch.autograd.Function):
@@ -425,21 +421,13 @@ class _StemFn(torch.autograd.Function):
         w, gamma, beta = stem.conv.weight, stem.bn.weight, stem.bn.bias
         (dg, dg_direct), (db, db_direct) = _gacc(gamma), _gacc(beta)
         do4 = dout.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
-        fused = False
-        if _STEM_FUSED_WG and ctx.pairs and yam is not None and r == 7 and (s + 1) // 2 == 4:
-            dwp = torch.empty(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)
-            fused = L.stem_bn_pool_bwd_wgrad(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, x8, dwp, dg, db, yam)
-        if fused:
-            pass
-        elif ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
-            dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db,
-                                     yam=yam)[0]
+        dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db,
+                                 yam=yam)[0]
+        if ctx.pairs:  # pair form: the stored input is [N, Hp, Wp/2, 8]
             dwp = torch.empty(k, r, (s + 1) // 2, 8, device=x8.device, dtype=torch.float32)  # beta 0: overwritten
             L.conv_wgrad(dy4, x8, dwp, 0.0, st, 0, stride_w=1, sched=_STEM_WG_SCHED,
                          target_wgs=_STEM_WG_WGS)
         else:
-            dy4 = L.stem_bn_pool_bwd(do4, idx, y4, gamma, beta, smean, sinv, *_POOL, dgamma_acc=dg, dbeta_acc=db,
-                                     yam=yam)[0]
             dwp = torch.empty(k, r, s, 8, device=x8.device, dtype=torch.float32)
             L.conv_wgrad(dy4, x8, dwp, 0.0, st, pad)
         grads = []
