@@ -120,6 +120,8 @@ def _wait_all(works):
 
 
 from ..utils.trace import traced  # noqa: E402
+from ..graph import Op  # noqa: E402
+from ..train.hooks import SessionRunHook  # noqa: E402
 
 
 def _group_payload_grads(flat):
@@ -343,6 +345,20 @@ class AsyncPSWorker:
         self.pushes += 1
         return True
 
+    # ---- session surface (train/eager.py): the reference's worker loop, sess.run(train_op) under a session ----------
+    def minimize(self, loss_fn, global_step=None, inputs=(), name="async_ps_train"):
+        """A train op for ``sess.run``: forward + backward of ``loss_fn(*inputs)``, then :meth:`step_done` (the
+        window's local optimizer step, and the push / pull every ``window`` steps) and ``global_step += 1`` -- the
+        worker loop of /root/reference/Hogwild/Hogwild.py:44-57 and DOWNPOUR/DOWNPOUR.py:116-140 with the
+        parameters in the PS's HBM.  ``global_step`` counts this worker's local steps (the PS counts updates)."""
+        from ..train.eager import EagerGradients
+        return _AsyncPSApply(EagerGradients(loss_fn, inputs, name + "/gradients"), self, global_step, name)
+
+    def make_session_run_hook(self):
+        """after_create_session: the initial pull (:meth:`begin`); end: :meth:`finish` (the PS's ``serve()``
+        returns once every worker finished, the ``Server.join()`` of the reference's PS task)."""
+        return _AsyncPSHook(self)
+
     def warm(self):
         """Tell the PS this worker has finished its warm-up (``AsyncPSServer.timed`` starts when all have)."""
         self._ann.submit(self.rank, _WARM)
@@ -362,6 +378,46 @@ class AsyncPSWorker:
             if "connection lost" not in str(e):
                 raise
         self._ctl.close()
+
+
+class _AsyncPSApply(Op):
+    """The worker's train op (AsyncPSWorker.minimize)."""
+
+    def __init__(self, grads, worker, global_step, name):
+        self.grads, self.worker, self.global_step = grads, worker, global_step
+        super().__init__(lambda c, *a: None, [grads], name)
+
+    def _eval(self, ctx):
+        ctx.eval(self.grads)
+        self.worker.step_done()
+        gs = self.global_step
+        if gs is not None:
+            with gs._lock:
+                gs._local.add_(1)
+        return None
+
+    @property
+    def loss(self):
+        """The step's loss as a fetchable tensor (fetching it synchronises the device)."""
+        return self.grads
+
+
+class _AsyncPSHook(SessionRunHook):
+    """AsyncPSWorker.make_session_run_hook: initial pull once the session exists, finish() at its end."""
+
+    def __init__(self, worker):
+        self.worker = worker
+        self._begun = False
+
+    def after_create_session(self, session, coord):
+        if not self._begun:
+            self.worker.begin()
+            self._begun = True
+
+    def end(self, session):
+        if self._begun:
+            self.worker.finish()
+            self._begun = False
 
 
 class AsyncPSServer:

@@ -21,7 +21,7 @@ import _path  # noqa: F401
 
 import torch
 
-import dtg  # noqa: F401
+import dtg
 from dtg import ops
 from dtg.models import resnet
 from dtg.optim import make_optimizer
@@ -71,24 +71,34 @@ def main():
         print(f"[ps] {n} updates in {dt:.1f}s, per worker {ps.per_worker}, mean staleness "
               f"{sum(st) / max(1, len(st)):.2f}", flush=True)
     else:
+        # the reference's worker loop (Hogwild/Hogwild.py:44-57): a train op run under a session until the stop
+        # hook fires; the session's hook does the initial pull and tells the PS when this worker is done
         local = make_optimizer(a.local_opt, flat, a.local_lr or a.lr) if a.window > 1 else None
         w = AsyncPSWorker(flat, ps_rank=0, window=a.window, window_mode=a.window_mode, local_optimizer=local,
                           overlap_pull=a.overlap_pull)
         dt_ = torch.bfloat16 if device.type == "cuda" else torch.float32
         x, y = resnet.synthetic_batch(a.batch, device, dt_, a.image, ncls, seed=rank)
-        w.begin()
+        images, labels = dtg.placeholder(name="images"), dtg.placeholder(name="labels")
+        global_step = dtg.train.get_or_create_global_step()
+        train_op = w.minimize(lambda xb, yb: ops.softmax_cross_entropy(model(xb), yb), global_step=global_step,
+                              inputs=(images, labels))
+        counter = dtg.train.StepCounterHook(every_n_steps=10, batch_size=a.batch)
+        hooks = [w.make_session_run_hook(), dtg.train.StopAtStepHook(last_step=a.steps), counter]
         t0 = time.time()
-        for i in range(a.steps):
-            loss = ops.softmax_cross_entropy(model(x), y)
-            loss.backward()
-            w.step_done()
-            if i % 10 == 0:
-                print(f"[worker {a.task_index}] step {i} loss {loss.item():.4f}", flush=True)
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.time() - t0
-        w.finish()
-        print(f"[worker {a.task_index}] {a.steps * a.batch / dt:.1f} images/sec", flush=True)
+        with dtg.train.MonitoredTrainingSession(is_chief=False, hooks=hooks, log_step_count_steps=None,
+                                                save_summaries_steps=None, save_checkpoint_secs=None) as sess:
+            step = 0
+            while not sess.should_stop():
+                if step % 10 == 0:
+                    _, loss, step = sess.run([train_op, train_op.loss, global_step], feed_dict={images: x, labels: y})
+                    print(f"[worker {a.task_index}] step {int(step) - 1} loss {float(loss):.4f}", flush=True)
+                else:
+                    _, step = sess.run([train_op, global_step], feed_dict={images: x, labels: y})
+                step = int(step)
+            if device.type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.time() - t0
+        print(f"[worker {a.task_index}] {a.steps * a.batch / dt:.1f} images/sec, {w.pushes} pushes", flush=True)
 
 
 if __name__ == "__main__":

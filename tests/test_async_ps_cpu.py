@@ -658,3 +658,36 @@ def test_bound_inflight_times_out_naming_the_worker(monkeypatch):
     ps._bound_inflight(3)
     with pytest.raises(TimeoutError, match="worker rank 3"):
         ps._bound_inflight(5)
+
+
+def test_resnet_async_ps_example_session_driven(tmp_path):
+    """examples/ResNet50/resnet50_async_ps.py (tiny ResNet, gloo): 1 PS + 2 workers, the workers' loop is a
+    MonitoredTrainingSession running AsyncPSWorker.minimize's train op until StopAtStepHook; the session's hook
+    pulls first and finishes the worker, and the PS's serve() returns after 2 x 4 updates."""
+    import subprocess
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cluster import free_ports
+    base = free_ports(1)[0]
+    script = os.path.join(ROOT, "examples", "ResNet50", "resnet50_async_ps.py")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", DTG_BACKEND="gloo")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    args = ["--tiny", "--workers", "2", "--steps", "4", "--batch", "2", "--image", "32", "--base_port", str(base)]
+    procs = [subprocess.Popen([sys.executable, script, "--job_name", "ps", "--task_index", "0"] + args, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)]
+    procs += [subprocess.Popen([sys.executable, script, "--job_name", "worker", "--task_index", str(i)] + args,
+                               env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for i in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            outs.append((p.returncode, o, e))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for rc, o, e in outs:
+        assert rc == 0, o + e[-3000:]
+    assert "[ps] 8 updates" in outs[0][1], outs[0][1]
+    for rc, o, e in outs[1:]:
+        assert "step 0 loss" in o and "4 pushes" in o, o
