@@ -257,8 +257,9 @@ std::vector<Tensor> attn_fused_fwd(Tensor qkv, c10::optional<Tensor> mask, int64
   return {out, lse};
 }
 
+// dbias (optional, fp32 [3 * nh * 64]): the QKV bias gradient is ADDED into it by the kernel's epilogue
 Tensor attn_fused_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, c10::optional<Tensor> mask, int64_t B,
-                      int64_t S, int64_t nh, double p, int64_t seed) {
+                      int64_t S, int64_t nh, double p, int64_t seed, c10::optional<Tensor> dbias) {
   CHECK_GPU_BF16_CONTIG(qkv);
   CHECK_GPU_BF16_CONTIG(out);
   CHECK_GPU_BF16_CONTIG(dout);
@@ -271,10 +272,15 @@ Tensor attn_fused_bwd(Tensor qkv, Tensor out, Tensor dout, Tensor lse, c10::opti
     CHECK_F32_CONTIG(*mask);
     TORCH_CHECK(mask->numel() == B * S, "mask must be [B, S]");
   }
+  if (has(dbias)) {
+    CHECK_F32_CONTIG(*dbias);
+    TORCH_CHECK(dbias->numel() == 3 * nh * 64 && dbias->device() == qkv.device(), "dbias must be fp32 [3 * nh * 64]");
+  }
   c10::DeviceGuard dg(qkv.device());
   auto dqkv = at::empty_like(qkv);
   dtg::attn_bwd(cbfp(qkv), cbfp(out), cbfp(dout), lse.data_ptr<float>(), has(mask) ? mask->data_ptr<float>() : nullptr,
-                bfp(dqkv), (int)B, (int)S, (int)nh, (float)p, (uint32_t)seed, cur_stream());
+                bfp(dqkv), (int)B, (int)S, (int)nh, (float)p, (uint32_t)seed,
+                has(dbias) ? dbias->data_ptr<float>() : nullptr, cur_stream());
   return dqkv;
 }
 
@@ -418,7 +424,9 @@ void register_transformer_ops(py::module_& m) {
         py::arg("nsel") = 1);
   m.def("emb_fwd", &emb_fwd);
   m.def("attn_fused_fwd", &attn_fused_fwd);
-  m.def("attn_fused_bwd", &attn_fused_bwd);
+  m.def("attn_fused_bwd", &attn_fused_bwd, py::arg("qkv"), py::arg("out"), py::arg("dout"), py::arg("lse"),
+        py::arg("mask"), py::arg("B"), py::arg("S"), py::arg("nh"), py::arg("p"), py::arg("seed"),
+        py::arg("dbias") = py::none());
   m.def("attn_fused_supported", [](int64_t S, int64_t dh, bool bwd) { return dtg::attn_fused_supported(S, dh, bwd) != 0; });
   m.def("emb_word_bwd", &emb_word_bwd);
   m.def("gather_rows", &gather_rows);

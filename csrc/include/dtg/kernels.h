@@ -207,7 +207,7 @@ int attn_fused_supported(int S, int dh, int backward);
 void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int B, int S, int nh, float p,
               uint32_t seed, hipStream_t st);
 void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, const float* mask,
-              bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, hipStream_t st);
+              bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, float* dbias, hipStream_t st);
 
 // ---- pooling, NHWC (pool.hip) -----------------------------------------------------------------
 void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int k, int s, int pad, int P,

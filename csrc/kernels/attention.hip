@@ -19,6 +19,9 @@
 //
 // Fragment conventions as in dtg/mfma_gemm.cuh: mfma(a = X_A[m][k], b = X_B[n][k]) accumulates
 // C[m][n], lane l holding C[(l>>4)*4 + r][l & 15].
+// dbias (optional, fp32 [3 * nh * 64]): the QKV bias gradient, column sums of dQ | dK | dV over all B * S rows,
+// added in the backward's epilogue (per-wave sums, combined over the workgroup in LDS, one device atomic per
+// column and workgroup) instead of a second pass over the 3H-wide dQKV.
 // The dropout element index is ((b*nh + h)*S + q)*S + key, identical to attn_softmax_fwd and to
 // the PyTorch mirror (dtg/ops/transformer.py) -- the fused and unfused paths agree bit-for-bit on
 // which probabilities are dropped.
@@ -66,6 +69,18 @@ __device__ __forceinline__ void st_bf16(lds_char* base, int off, float v) {
 }
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Column sums of a wave's 16 C-layout rows x 64 columns (v * scale): the lane's 4 rows, then the 4 lane groups
+// that share a column (xor 16, 32).  Lanes 0-15 hold columns j * 16 + lane.
+__device__ __forceinline__ void colsum16(const f32x4 (&v)[4], float scale, float (&s)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float t = (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    s[j] = t * scale;
+  }
+}
 
 }  // namespace
 
@@ -239,7 +254,8 @@ template <int S_>
 __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ o,
                                                        const bf16_t* __restrict__ dout, const float* __restrict__ lse,
                                                        const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
-                                                       int nh, float scale, uint32_t th, float dscale, uint32_t seed) {
+                                                       int nh, float scale, uint32_t th, float dscale, uint32_t seed,
+                                                       float* __restrict__ dbias) {
   constexpr int S = S_, NW = 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
@@ -373,6 +389,22 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
     for (int c = 0; c < S / 64; ++c) stage_mc<64, DenseMC<false>, NW>(kss, Kt + c * 8192, 0, c * 64, wave, lane);
   }
   lds_char* stg = dOt + wave * 2048;  // per-wave output staging inside the dO tile (16 or 32 KB)
+  // bias-gradient partials: the wave's [dQ | dK | dV] column sums in its (now idle) P scratch
+  lds_float* bsum = reinterpret_cast<lds_float*>(scr);
+  if (dbias) {
+    float sk[4] = {0.f, 0.f, 0.f, 0.f}, sv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (has_keys) {
+      colsum16(dk, scale, sk);
+      colsum16(dv, 1.f, sv);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bsum[64 + j * 16 + lane] = sk[j];
+        bsum[128 + j * 16 + lane] = sv[j];
+      }
+    }
+  }
   if (has_keys) {
     bf16_t* gk = dqkv + ((long long)b * S + kb) * ld + H + h * 64;
     store_rows16(stg, dk, scale, gk, ld, lane);
@@ -397,6 +429,26 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
                                                         dq[j], 0, 0, 0);
     }
     store_rows16(stg, dq, scale, dqkv + ((long long)b * S + qr) * ld + h * 64, ld, lane);
+    if (dbias) {
+      float sq[4];
+      colsum16(dq, scale, sq);
+      if (lane < 16)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bsum[j * 16 + lane] = sq[j];
+    }
+  } else if (dbias && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bsum[j * 16 + lane] = 0.f;
+  }
+  if (dbias) {  // (kernel argument: uniform) 8 wave partials -> one atomic per column
+    __syncthreads();
+    if (tid < 192) {
+      const int part = tid >> 6, c = tid & 63;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += reinterpret_cast<lds_float*>(Ms + S)[w * 256 + tid];
+      atomicAdd(dbias + part * H + h * 64 + c, t);
+    }
   }
 }
 
@@ -434,7 +486,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_kernel(const bf16_t* __restr
                                                            const float* __restrict__ lse,
                                                            const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
                                                            int S, int nh, float scale, uint32_t th, float dscale,
-                                                           uint32_t seed) {
+                                                           uint32_t seed, float* __restrict__ dbias) {
   constexpr int NW = 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
@@ -557,6 +609,17 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_kernel(const bf16_t* __restr
     bf16_t* gk = dqkv + ((long long)b * S + kb) * ld + H + h * 64;
     store_rows16(stg, dk, scale, gk, ld, lane);
     store_rows16(stg, dv, 1.f, gk + H, ld, lane);
+    if (dbias) {  // (long sequences: one device atomic per column and wave)
+      float sk[4], sv[4];
+      colsum16(dk, scale, sk);
+      colsum16(dv, 1.f, sv);
+      if (lane < 16)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(dbias + H + h * 64 + j * 16 + lane, sk[j]);
+          atomicAdd(dbias + 2 * H + h * 64 + j * 16 + lane, sv[j]);
+        }
+    }
   }
 }
 
@@ -564,7 +627,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_kernel(const bf16_t* __restri
                                                           const bf16_t* __restrict__ dout, const float* __restrict__ lse,
                                                           const float* __restrict__ mask, bf16_t* __restrict__ dqkv,
                                                           int S, int nh, float scale, uint32_t th, float dscale,
-                                                          uint32_t seed) {
+                                                          uint32_t seed, float* __restrict__ dbias) {
   constexpr int NW = 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
@@ -666,6 +729,13 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_kernel(const bf16_t* __restri
     lds_fence();  // the scratch is rewritten by the next chunk
   }
   store_rows16(scr, dq, scale, dqkv + ((long long)b * S + q0) * ld + h * 64, ld, lane);
+  if (dbias) {
+    float sq[4];
+    colsum16(dq, scale, sq);
+    if (lane < 16)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(dbias + h * 64 + j * 16 + lane, sq[j]);
+  }
 }
 
 static uint32_t drop_th(float p) {
@@ -700,7 +770,7 @@ void attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse, int
 }
 
 void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const float* lse, const float* mask,
-              bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, hipStream_t st) {
+              bf16_t* dqkv, int B, int S, int nh, float p, uint32_t seed, float* dbias, hipStream_t st) {
   const uint32_t th = drop_th(p);
   const float ds = p > 0.f ? 1.f / (1.f - p) : 1.f;
   static bool attr = false;
@@ -716,15 +786,15 @@ void attn_bwd(const bf16_t* qkv, const bf16_t* o, const bf16_t* dout, const floa
   if (S > 128) {
     const dim3 grid(B * nh, (S + kLongKeys - 1) / kLongKeys);
     hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(512), dkv_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                       0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+                       0.125f, th, ds, seed, dbias); DTG_LAUNCH_CHECK();
     hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(512), dq_lds(S), st, qkv, o, dout, lse, mask, dqkv, S, nh,
-                       0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+                       0.125f, th, ds, seed, dbias); DTG_LAUNCH_CHECK();
   } else if (S == 64) {
     hipLaunchKernelGGL(attn_bwd_kernel<64>, dim3(B * nh), dim3(512), bwd_lds(64), st, qkv, o, dout, lse, mask, dqkv,
-                       nh, 0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+                       nh, 0.125f, th, ds, seed, dbias); DTG_LAUNCH_CHECK();
   } else {
     hipLaunchKernelGGL(attn_bwd_kernel<128>, dim3(B * nh), dim3(512), bwd_lds(128), st, qkv, o, dout, lse, mask,
-                       dqkv, nh, 0.125f, th, ds, seed); DTG_LAUNCH_CHECK();
+                       dqkv, nh, 0.125f, th, ds, seed, dbias); DTG_LAUNCH_CHECK();
   }
 }
 

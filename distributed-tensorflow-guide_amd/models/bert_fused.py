@@ -33,6 +33,8 @@ _ATTN = "fused"  # "fused" (attention.hip) or "gemm" (batched GEMMs + softmax; A
 # split-K workgroup target of the weight gradients when they run on the side stream (parallel/overlap.py); 0 = the
 # GEMM's own default (512).  Module switch for the A/B tools (tools/bench_cfg.py DTG_AB_SET).
 _WSPLIT_WGS = 0
+# QKV bias gradient from the fused attention backward's epilogue (True) or a separate column-sum pass (A/B switch)
+_FUSED_DBIAS = True
 _wsplit_cache = {}
 
 
@@ -131,12 +133,16 @@ class _LayerFn(torch.autograd.Function):
         with overlap.wgrad_scope(dao, cx):
             _wgrad(dao, cx, gw_o)
         dcx = gemm(dao, True, w_o, False)
-        if ctx.fused_attn:
-            dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a)
+        if ctx.fused_attn and _FUSED_DBIAS and gb_qkv.dtype == torch.float32 and gb_qkv.is_contiguous():
+            # the QKV bias gradient (column sums of dQKV) is added by the attention backward's epilogue
+            dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a, gb_qkv)
         else:
-            dqkv = torch.empty_like(qkv)
-            T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
-        L.colsum(dqkv, gb_qkv, True)
+            if ctx.fused_attn:
+                dqkv = L.attn_fused_bwd(qkv, cx, dcx, P, ctx.mask_add, B, S, nh, p_a, s_a)
+            else:
+                dqkv = torch.empty_like(qkv)
+                T.attention_bwd(dcx, qkv, P, Pd, B, S, nh, dqkv)
+            L.colsum(dqkv, gb_qkv, True)
         with overlap.wgrad_scope(dqkv, x):
             _wgrad(dqkv, x, gw_qkv)
         if p_h <= 0:

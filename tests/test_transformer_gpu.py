@@ -263,6 +263,13 @@ def test_fused_attention_fwd_bwd(S, p):
     for i, name in enumerate("qkv"):
         a, r = dqkv[:, i * H:(i + 1) * H], qr.grad[:, i * H:(i + 1) * H]
         assert rel(a, r) < 3e-2, (name, rel(a, r))
+    # the fused QKV bias gradient: added into an existing fp32 buffer, same dQKV as without it
+    db = torch.full((3 * H,), 0.5, device=dev)
+    dqkv2 = lib().attn_fused_bwd(qkv, out, dout, lse, mask, B, S, nh, p, 1234, db)
+    assert torch.equal(dqkv2, dqkv)
+    ref_db = qr.grad.sum(0) + 0.5
+    assert rel(db, ref_db) < 2e-2, rel(db, ref_db)
+    assert torch.allclose(db, dqkv.float().sum(0) + 0.5, atol=0.05 * dqkv.float().sum(0).abs().max().item() + 1e-3)
 
 
 @pytest.mark.parametrize("S", [256, 512])
