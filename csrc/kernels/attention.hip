@@ -4,10 +4,10 @@
 // Forward  (grid: [B*nh, ceil(S/128)], 8 waves; a wave owns 16 query rows, a workgroup 128 queries):
 //   K and V of the (b, h) are staged once per 128 queries (once per head at S = 128) into LDS by LDS-DMA (K row-major/KC, V as k-major MC
 //   tiles read back with ds_read_b64_tr_b16); Q fragments come straight from global memory.  Per
-//   64-key chunk: S = Q K^T (8 MFMA) -> scale + mask -> online softmax (running max / sum per row,
-//   reductions across the 16 lanes that share a row) -> dropout(P) through a per-wave LDS
-//   scratch into A-fragment layout -> O += P V (8 MFMA).  Writes O (bf16, coalesced through LDS) and
-//   LSE = m + log(l) per row for the backward.  No [S, S] matrix ever reaches HBM.
+//   64-key chunk, transposed: S^T = K Q^T (8 MFMA; a lane holds one query x 4 consecutive keys per block) ->
+//   scale + mask -> online softmax (per-lane running max / sum; two cross-lane steps for the chunk max) ->
+//   dropout(P) through a per-wave LDS scratch (one 8-byte store per block) -> O^T += V^T P^T (8 MFMA).  Writes O
+//   (bf16, coalesced through LDS) and LSE = m + log(l) per row for the backward.  No [S, S] matrix reaches HBM.
 // Backward (grid: [B*nh], 8 waves; a wave owns 16 keys; S in {64, 128}; longer S: two launches, below):
 //   recomputes P^T = exp(K Q^T * scale + mask - LSE) per 32-query chunk, then
 //   dV += dropout(P)^T dO,  dP^T = V dO^T,  dS^T = P^T (dropout'(dP^T) - D),  dK += dS^T Q * scale;
@@ -22,9 +22,9 @@
 // dbias (optional, fp32 [3 * nh * 64]): the QKV bias gradient, column sums of dQ | dK | dV over all B * S rows,
 // added in the backward's epilogue (per-wave sums, combined over the workgroup in LDS, one device atomic per
 // column and workgroup) instead of a second pass over the 3H-wide dQKV.
-// The dropout element index is ((b*nh + h)*S + q)*S + key, identical to attn_softmax_fwd and to
-// the PyTorch mirror (dtg/ops/transformer.py) -- the fused and unfused paths agree bit-for-bit on
-// which probabilities are dropped.
+// The dropout element index is ((b*nh + h)*S + q)*S + key, drawn by the pair hash (keep_attn below), identical to
+// attn_softmax_fwd and to the PyTorch mirror (dtg/ops/transformer.py attn_dropout_keep) -- the fused and unfused
+// paths agree bit-for-bit on which probabilities are dropped.
 #include "dtg/common.h"
 #include "dtg/kernels.h"
 #include "dtg/mfma_gemm.cuh"
@@ -42,8 +42,21 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   return h;
 }
-__device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t idx, uint32_t thresh) {
-  return fmix32(idx * 0x9E3779B1u + seed) >= thresh;
+// Attention-probability dropout: ONE hash per pair of adjacent keys.  Element idx (= ((b*nh + h)*S + q)*S + key)
+// is kept iff the low (even idx) / high (odd idx) 16 bits of fmix32((idx >> 1) * golden + seed) are >= th16 =
+// floor(p * 2^16): half the hashes of a per-element draw, and the kernels hold 4 consecutive keys per lane.
+__device__ __forceinline__ uint32_t pair_hash(uint32_t seed, uint32_t pidx) { return fmix32(pidx * 0x9E3779B1u + seed); }
+__device__ __forceinline__ bool keep_attn(uint32_t seed, uint32_t idx, uint32_t th16) {
+  const uint32_t h = pair_hash(seed, idx >> 1);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xffffu)) >= th16;
+}
+// keep flags of 4 consecutive keys starting at an even idx
+__device__ __forceinline__ void keep4_attn(uint32_t seed, uint32_t idx0, uint32_t th16, bool (&k)[4]) {
+  const uint32_t h0 = pair_hash(seed, idx0 >> 1), h1 = pair_hash(seed, (idx0 >> 1) + 1u);
+  k[0] = (h0 & 0xffffu) >= th16;
+  k[1] = (h0 >> 16) >= th16;
+  k[2] = (h1 & 0xffffu) >= th16;
+  k[3] = (h1 >> 16) >= th16;
 }
 
 // 16 B of a KC row straight from global memory (A/B fragment of a [rows][64] operand)
@@ -126,16 +139,17 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (!active) return;  // (no barrier below this point)
-  float m[4], l[4];
+  // Transposed form: S^T = K Q^T and O^T = V^T P^T, so lane (q = lane & 15, g = lane >> 4) holds, per 16-key block
+  // j, the scores of ONE query q0 + q against 4 consecutive keys j * 16 + 4g + [0, 4): the softmax statistics are
+  // per lane (running max / sum need 2 cross-lane steps per chunk for the max and one final sum, not 4 rows x 4
+  // steps each), the dropout pairs are in-lane (2 hashes per 4 keys), P leaves as one 8-byte LDS store per block,
+  // and O^T's accumulators (4 consecutive d per block) rescale by the lane's own alpha.
+  float m = -INFINITY, l = 0.f;  // l: this lane's partial sum (its 16 of every 64 keys), combined at the end
   f32x4 o[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-  }
-#pragma unroll
   for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int rbase = (lane >> 4) * 4;  // this lane's 4 C rows
+  const int qi = lane & 15, g = lane >> 4;
+  const uint32_t qrow = ((uint32_t)bh * (uint32_t)S + (uint32_t)(q0 + qi)) * (uint32_t)S;  // dropout index base
   for (int kc = 0; kc < nkc; ++kc) {
     f32x4 s[4];
 #pragma unroll
@@ -143,73 +157,67 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
       s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], frag_kc(Kt + kc * 8192, j * 16, ks, lane), s[j], 0, 0, 0);
+        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_kc(Kt + kc * 8192, j * 16, ks, lane), qa[ks], s[j], 0, 0, 0);
     }
-    float mx[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
+    float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float madd = Mk[kc * 64 + j * 16 + (lane & 15)];
+      const f32x4 madd = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(Mk + kc * 64 + j * 16 + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        s[j][r] = s[j][r] * scale + madd;
-        mx[r] = fmaxf(mx[r], s[j][r]);
+        s[j][r] = fmaf(s[j][r], scale, madd[r]);
+        mx = fmaxf(mx, s[j][r]);
       }
     }
-    float alpha[4], rs[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o_ = 1; o_ < 16; o_ <<= 1) mx[r] = fmaxf(mx[r], __shfl_xor(mx[r], o_, 64));
-      const float mn = fmaxf(m[r], mx[r]);
-      alpha[r] = __expf(m[r] - mn);
-      m[r] = mn;
-      rs[r] = 0.f;
-    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    m = mn;
+    float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int key = kc * 64 + j * 16 + (lane & 15);
+      const int key0 = kc * 64 + j * 16 + 4 * g;
+      float pd[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = __expf(s[j][r] - m[r]);
-        rs[r] += p;
-        float pd = p;
-        if (th) {
-          const uint32_t idx = ((uint32_t)bh * (uint32_t)S + (uint32_t)(q0 + rbase + r)) * (uint32_t)S + (uint32_t)key;
-          pd = keep_elem(seed, idx, th) ? p * dscale : 0.f;
-        }
-        st_bf16(scr, kc_off(rbase + r, j * 16 + (lane & 15)), pd);
+        pd[r] = __expf(s[j][r] - mn);
+        rs += pd[r];
       }
+      if (th) {
+        const uint32_t pidx = (qrow + (uint32_t)key0) >> 1;
+        const uint32_t h0 = pair_hash(seed, pidx), h1 = pair_hash(seed, pidx + 1u);
+        pd[0] = (h0 & 0xffffu) >= th ? pd[0] * dscale : 0.f;
+        pd[1] = (h0 >> 16) >= th ? pd[1] * dscale : 0.f;
+        pd[2] = (h1 & 0xffffu) >= th ? pd[2] * dscale : 0.f;
+        pd[3] = (h1 >> 16) >= th ? pd[3] * dscale : 0.f;
+      }
+      st4_bf16(scr + kc_off(qi, j * 16 + 4 * g), pd);  // P [16 q][64 keys] KC: 4 keys in one 16-B chunk
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int o_ = 1; o_ < 16; o_ <<= 1) rs[r] += __shfl_xor(rs[r], o_, 64);
-      l[r] = l[r] * alpha[r] + rs[r];
-    }
+    l = l * alpha + rs;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
+      for (int r = 0; r < 4; ++r) o[j][r] *= alpha;
     lds_fence();
-    v8bf pa0 = frag_kc(scr, 0, 0, lane), pa1 = frag_kc(scr, 0, 1, lane);
+    const v8bf pb0 = frag_kc(scr, 0, 0, lane), pb1 = frag_kc(scr, 0, 1, lane);  // X_B[q][key]
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa0, frag_mc<64>(Vt + kc * 8192, j * 16, 0, lane), o[j], 0, 0, 0);
-      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa1, frag_mc<64>(Vt + kc * 8192, j * 16, 1, lane), o[j], 0, 0, 0);
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_mc<64>(Vt + kc * 8192, j * 16, 0, lane), pb0, o[j], 0, 0, 0);
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_mc<64>(Vt + kc * 8192, j * 16, 1, lane), pb1, o[j], 0, 0, 0);
     }
     lds_fence();  // the scratch is rewritten by the next chunk
   }
-  // finalize: O / l -> scratch (plain row-major [16][64]) -> 16-B global stores
+  // finalize: O^T / l -> scratch (row-major [16 q][64 d], 4 consecutive d per lane and block) -> 16-B global stores
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float il = 1.f / l;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) st_bf16(scr, (rbase + r) * 128 + (j * 16 + (lane & 15)) * 2, o[j][r] / l[r]);
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) lse[(long long)bh * S + q0 + rbase + r] = m[r] + __logf(l[r]);
+  for (int j = 0; j < 4; ++j) {
+    const float v[4] = {o[j][0] * il, o[j][1] * il, o[j][2] * il, o[j][3] * il};
+    st4_bf16(scr + qi * 128 + (j * 16 + 4 * g) * 2, v);
   }
+  if (g == 0) lse[(long long)bh * S + q0 + qi] = m + __logf(l);
   lds_fence();
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -353,14 +361,15 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16_t* __restrict_
         const float lq = Ls[q] * kLog2e, dq = Ds[q];
         const uint32_t ib = ((uint32_t)bh * (uint32_t)S + (uint32_t)q) * (uint32_t)S + (uint32_t)(kb + rbase);
         float pd[4], dsv[4];
+        bool kp[4] = {true, true, true, true};
+        if (th) keep4_attn(seed, ib, th, kp);  // ib even: kb + rbase is a multiple of 4
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], sl2, msl[r] - lq));
           float pv = p, dp = dpt[ni][r];
           if (th) {
-            const bool kp = keep_elem(seed, ib + r, th);
-            pv = kp ? p * dscale : 0.f;
-            dp = kp ? dp * dscale : 0.f;
+            pv = kp[r] ? p * dscale : 0.f;
+            dp = kp[r] ? dp * dscale : 0.f;
           }
           pd[r] = pv;
           dsv[r] = p * (dp - dq);
@@ -575,14 +584,15 @@ __global__ void __launch_bounds__(512) attn_bwd_dkv_kernel(const bf16_t* __restr
         const float lq = Ls[q] * kLog2e, dq = Ds[q];
         const uint32_t ib = ((uint32_t)bh * (uint32_t)S + (uint32_t)q) * (uint32_t)S + (uint32_t)(kb + rbase);
         float pd[4], dsv[4];
+        bool kp[4] = {true, true, true, true};
+        if (th) keep4_attn(seed, ib, th, kp);  // ib even: kb + rbase is a multiple of 4
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = __builtin_amdgcn_exp2f(fmaf(st[ni][r], sl2, msl[r] - lq));
           float pv = p, dp = dpt[ni][r];
           if (th) {
-            const bool kp = keep_elem(seed, ib + r, th);
-            pv = kp ? p * dscale : 0.f;
-            dp = kp ? dp * dscale : 0.f;
+            pv = kp[r] ? p * dscale : 0.f;
+            dp = kp[r] ? dp * dscale : 0.f;
           }
           pd[r] = pv;
           dsv[r] = p * (dp - dq);
@@ -714,7 +724,7 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_kernel(const bf16_t* __restri
         float dpv = dp[j][r];
         if (th) {
           const uint32_t idx = ((uint32_t)bh * (uint32_t)S + (uint32_t)(q0 + rbase + r)) * (uint32_t)S + (uint32_t)key;
-          dpv = keep_elem(seed, idx, th) ? dpv * dscale : 0.f;
+          dpv = keep_attn(seed, idx, th) ? dpv * dscale : 0.f;
         }
         st_bf16(scr, kc_off(rbase + r, j * 16 + (lane & 15)), p * (dpv - dd[r]));
       }
@@ -738,10 +748,11 @@ __global__ void __launch_bounds__(512) attn_bwd_dq_kernel(const bf16_t* __restri
   }
 }
 
+// 16-bit threshold of the pair-hash dropout (keep_attn); 0 = no dropout
 static uint32_t drop_th(float p) {
   if (p <= 0.f) return 0u;
-  const double t = (double)p * 4294967296.0;
-  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const double t = (double)p * 65536.0;
+  return t >= 65535.0 ? 0xffffu : (t < 1.0 ? 1u : (uint32_t)t);
 }
 
 int attn_fused_supported(int S, int dh, int backward) {

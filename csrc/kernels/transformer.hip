@@ -29,6 +29,18 @@ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 __device__ __forceinline__ bool keep_elem(uint32_t seed, uint32_t idx, uint32_t thresh) {
   return fmix32(idx * 0x9E3779B1u + seed) >= thresh;
 }
+// attention-probability dropout (the fused kernels' pair hash, attention.hip keep_attn): element idx is kept iff the
+// low (even idx) / high (odd idx) 16 bits of fmix32((idx >> 1) * golden + seed) are >= floor(p * 2^16).  Python
+// mirror: dtg/ops/transformer.py::attn_dropout_keep.
+__device__ __forceinline__ bool keep_attn(uint32_t seed, uint32_t idx, uint32_t th16) {
+  const uint32_t h = fmix32((idx >> 1) * 0x9E3779B1u + seed);
+  return ((idx & 1u) ? (h >> 16) : (h & 0xffffu)) >= th16;
+}
+static inline uint32_t drop_thresh16(float p) {
+  if (p <= 0.f) return 0u;
+  const double t = (double)p * 65536.0;
+  return t >= 65535.0 ? 0xffffu : (t < 1.0 ? 1u : (uint32_t)t);
+}
 static inline uint32_t drop_thresh(float p) {
   if (p <= 0.f) return 0u;
   const double t = (double)p * 4294967296.0;
@@ -315,7 +327,7 @@ __global__ void __launch_bounds__(256) attn_softmax_fwd_kernel(const float* __re
     if (c < Sk) {
       const float p = v[j] * inv;
       P[base + c] = f2bf(p);
-      if (Pd != P) Pd[base + c] = keep_elem(seed, (uint32_t)(base + c), th) ? f2bf(p * scl) : (bf16_t)0;
+      if (Pd != P) Pd[base + c] = keep_attn(seed, (uint32_t)(base + c), th) ? f2bf(p * scl) : (bf16_t)0;
     }
   }
 }
@@ -559,7 +571,7 @@ int attn_max_keys() { return 64 * 16; }
 void attn_softmax_fwd(const float* sc, const float* mask, bf16_t* P, bf16_t* Pd, int rows, int rows_per_b, int Sk,
                       float p, uint32_t seed, hipStream_t st) {
   if (rows <= 0) return;
-  const uint32_t th = drop_thresh(p);
+  const uint32_t th = drop_thresh16(p);
   const float scl = p > 0.f ? 1.f / (1.f - p) : 1.f;
   if (!th) Pd = P;
   const int nj = (Sk + 63) / 64;

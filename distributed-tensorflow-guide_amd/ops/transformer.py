@@ -5,8 +5,10 @@ The mirrors define the semantics the kernels must reproduce (tests compare the t
 * ``dropout_keep``   -- the counter-hash dropout mask: element ``i`` of a tensor is kept iff
   ``fmix32(i * 0x9E3779B1 + seed) >= floor(p * 2**32)``.  The kernels regenerate it in backward,
   so no mask tensor is ever stored.
+* ``attn_dropout_keep`` -- the attention-probability dropout: one hash per PAIR of adjacent elements, its
+  low / high 16 bits against ``floor(p * 2**16)`` (the fused attention kernels hold 4 consecutive keys per lane).
 * ``layer_norm_ref`` -- ``y = dropout_out(LN(res + dropout_in(h)))``.
-* ``attention_ref``  -- softmax(QK^T/sqrt(d) + mask) -> dropout -> @V per head.
+* ``attention_ref``  -- softmax(QK^T/sqrt(d) + mask) -> attention dropout -> @V per head.
 
 Not in the reference (TF1 toy models); this is the BERT-base slice of BASELINE.json
 config 5.
@@ -44,6 +46,34 @@ def dropout_keep(seed, numel, p, device=None):
     return h >= th
 
 
+def attn_drop_threshold(p):
+    """16-bit threshold of the attention-probability dropout (0 = off)."""
+    if p <= 0:
+        return 0
+    t = int(p * 65536.0)
+    return 0xFFFF if p * 65536.0 >= 65535.0 else max(t, 1)
+
+
+def attn_dropout_keep(seed, numel, p, device=None):
+    """Keep-mask of the attention-probability dropout, identical to attention.hip ``keep_attn`` and
+    transformer.hip ``attn_softmax_fwd``: one hash per pair of adjacent elements, element ``i`` kept iff the
+    low (even ``i``) / high (odd ``i``) 16 bits of ``fmix32((i >> 1) * 0x9E3779B1 + seed)`` are >= floor(p * 2**16)."""
+    th = attn_drop_threshold(p)
+    if th == 0:
+        return torch.ones(numel, dtype=torch.bool, device=device)
+    idx = torch.arange(numel, dtype=torch.int64, device=device)
+    h = _fmix32((((idx >> 1) * 0x9E3779B1) + (seed & _M32)) & _M32)
+    half = torch.where((idx & 1) == 1, h >> 16, h & 0xFFFF)
+    return half >= th
+
+
+def attn_dropout_ref(x, p, seed):
+    if p <= 0:
+        return x
+    keep = attn_dropout_keep(seed, x.numel(), p, x.device).view(x.shape)
+    return torch.where(keep, x / (1.0 - p), torch.zeros((), dtype=x.dtype, device=x.device))
+
+
 def dropout_ref(x, p, seed):
     if p <= 0:
         return x
@@ -70,7 +100,7 @@ def attention_ref(qkv, mask_add, B, S, nh, p=0.0, seed=0):
     if mask_add is not None:
         sc = sc + mask_add.view(B, 1, 1, S).to(sc.dtype)
     pr = torch.softmax(sc, dim=-1)
-    pr = dropout_ref(pr.reshape(-1, S), p, seed).view(B, nh, S, S)
+    pr = attn_dropout_ref(pr.reshape(-1, S), p, seed).view(B, nh, S, S)
     return (pr @ v).permute(0, 2, 1, 3).reshape(B * S, H)
 
 

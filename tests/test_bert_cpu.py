@@ -34,6 +34,29 @@ def test_dropout_hash_matches_scalar_definition():
         assert bool(keep[i]) == (fmix((i * 0x9E3779B1 + seed) & 0xFFFFFFFF) >= th)
 
 
+def test_attention_dropout_pair_hash():
+    """Attention-probability dropout: one fmix32 per pair of adjacent elements, low / high 16 bits against
+    floor(p * 2^16) (the fused kernels hold 4 consecutive keys per lane: 2 hashes instead of 4)."""
+    def fmix(h):
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+        h ^= h >> 13
+        h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+        return h ^ (h >> 16)
+    seed, p = 0x1234567, 0.1
+    th = int(p * 2 ** 16)
+    keep = T.attn_dropout_keep(seed, 4000, p)
+    for i in range(0, 4000, 29):
+        h = fmix(((i >> 1) * 0x9E3779B1 + seed) & 0xFFFFFFFF)
+        assert bool(keep[i]) == (((h >> 16) if i & 1 else (h & 0xFFFF)) >= th)
+    big = T.attn_dropout_keep(99, 400000, 0.1).float()
+    assert abs(big.mean().item() - 0.9) < 0.003
+    # the two halves of a pair are (close to) independent draws
+    ev, od = big[0::2], big[1::2]
+    assert abs((ev * od).mean().item() - ev.mean().item() * od.mean().item()) < 0.003
+    assert T.attn_dropout_keep(5, 10, 0.0).all()
+
+
 def test_layer_norm_ref_matches_torch():
     x = torch.randn(10, 48)
     r = torch.randn(10, 48)

@@ -131,7 +131,7 @@ def test_attention_softmax(S, p):
     scr = sc.clone().requires_grad_()
     pr = torch.softmax(scr.view(B, nh * S, S) + mask.view(B, 1, S), -1).view(-1, S)
     assert rel(P, pr) < 1e-2
-    pdr = T.dropout_ref(pr, p, 77)
+    pdr = T.attn_dropout_ref(pr, p, 77)
     assert rel(Pd, pdr) < 1e-2
     dPd = torch.randn_like(sc)
     pdr.backward(dPd)
