@@ -1,5 +1,5 @@
 // Streaming "expand" GEMM + BatchNorm statistics: C[M, N] = A[M, K] W[N, K]^T with the per-channel sum and
-// sum of squares of the stored (bf16-rounded) outputs, for short reductions (K = 64 / 128) into wide outputs
+// sum of squares of the stored (bf16-rounded) outputs, for short reductions (K = 64 / 128 / 256) into wide outputs
 // (N a multiple of 256): ResNet-50's conv3 / projection 1x1 convs of stages 1-2 (3211264 x 256 x 64 and
 // 802816 x 512 x 128 at batch 1024), whose time is the output write, not the MFMAs.
 //
@@ -320,10 +320,17 @@ __global__ void __launch_bounds__(256, 2) stem_stream_bn_kernel(const bf16_t* __
 
 }  // namespace
 
+// K = 256 (ResNet-50's stage-3 conv3, 200704 x 1024 x 256 at batch 1024, 64x256 tiles at 2.6 TB/s before): the
+// same kernel with a 96 KB ring (one workgroup per CU) and 128 VGPRs of weights per lane.  Switch for the A/B tools.
+static int g_expand_k256 = 1;
+void gemm_expand_k256_set(int on) { g_expand_k256 = on; }
+
 // false (nothing launched): not a shape this kernel serves, the caller takes the tiled path
 bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long ldw, bf16_t* C, long long ldc, int M,
                     int N, int K, float* part, hipStream_t st, int variant) {
-  if ((K != 64 && K != 128) || N % 256 || M % kXR || (lda & 7) || (ldw & 7) || (ldc & 7)) return false;
+  if ((K != 64 && K != 128 && !(K == 256 && g_expand_k256)) || N % 256 || M % kXR || (lda & 7) || (ldw & 7) ||
+      (ldc & 7))
+    return false;
   if ((long long)M * N < (1LL << 24)) return false;  // small problems: the tiled path fills the chip better
   const int nslice = N / 256;
   if (nslice & (nslice - 1)) return false;  // 1, 2, 4, ... (grid divisibility)
@@ -336,6 +343,8 @@ bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long l
     if (variant == 1) launch(gemm_expand_bn_kernel<64, true, 0>, expand_grid<64, true, 0>(nslice));
     else if (variant == 2) launch(gemm_expand_bn_kernel<64, false, 3>, expand_grid<64, false, 3>(nslice));
     else launch(gemm_expand_bn_kernel<64, false, 0>, expand_grid<64, false, 0>(nslice));
+  } else if (K == 256) {
+    launch(gemm_expand_bn_kernel<256, false, 0>, expand_grid<256, false, 0>(nslice));
   } else {
     if (variant == 1) launch(gemm_expand_bn_kernel<128, true, 0>, expand_grid<128, true, 0>(nslice));
     else if (variant == 2) launch(gemm_expand_bn_kernel<128, false, 2>, expand_grid<128, false, 2>(nslice));

@@ -55,10 +55,10 @@ def test_gemm_bn_fwd_stats(M, N, K):
     assert _rel(q, (of * of).sum(0)) < 1e-3
 
 
-# the persistent streaming expand kernel (csrc/kernels/gemm_expand.hip: K in {64, 128}, N % 256 == 0, M % 64 == 0,
-# M * N >= 2^24): one, two and four 256-column slices, a row-block count that does not divide the grid
+# the persistent streaming expand kernel (csrc/kernels/gemm_expand.hip: K in {64, 128, 256}, N % 256 == 0,
+# M % 64 == 0, M * N >= 2^24): one, two and four 256-column slices, a row-block count that does not divide the grid
 @pytest.mark.parametrize("M,N,K", [(65536, 256, 64), (32768, 512, 128), (64 * 1031, 256, 64), (16384, 1024, 64),
-                                   (20480, 1024, 128)])
+                                   (20480, 1024, 128), (16384, 1024, 256), (64 * 1031, 256, 256), (32768, 512, 256)])
 def test_gemm_bn_expand_stats(M, N, K):
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(1)

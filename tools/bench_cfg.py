@@ -11,6 +11,7 @@ so the choice is passed as DTG_AB_BN_CFG / DTG_AB_GEMM_CFG and applied here befo
     DTG_AB_HALO_WGRAD=0 python tools/bench_cfg.py     # the implicit-GEMM stage-1 3x3 wgrad instead of the halo one
     DTG_AB_LIN_WGRAD=0 python tools/bench_cfg.py      # the implicit-GEMM stage-2..4 3x3 wgrads instead of the linear halo
     DTG_AB_LIN_WGRAD=256 python tools/bench_cfg.py    # the linear-halo wgrads on 256 workgroups (halo: DTG_AB_HALO_WGRAD=128)
+    DTG_AB_EXPAND256=0 python tools/bench_cfg.py      # stage-3 conv3 (K = 256) on the tiled BN GEMM, not the expand kernel
 """
 import os
 import runpy
@@ -32,6 +33,8 @@ if os.environ.get("DTG_AB_HALO_WGRAD"):  # 0: the implicit-GEMM wgrad for the st
     lib().conv_halo_wgrad_set(int(os.environ["DTG_AB_HALO_WGRAD"]))
 if os.environ.get("DTG_AB_LIN_WGRAD"):  # 0: the implicit-GEMM wgrad for the stage-2..4 3x3s (conv_halo.hip lin)
     lib().conv_lin_wgrad_set(int(os.environ["DTG_AB_LIN_WGRAD"]))
+if os.environ.get("DTG_AB_EXPAND256"):  # 0: the tiled BN-statistics GEMM for K = 256 (stage-3 conv3) instead of expand
+    lib().gemm_expand_k256_set(int(os.environ["DTG_AB_EXPAND256"]))
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
