@@ -488,6 +488,11 @@ void conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, 
   if (bn.mode == 1 && R == 3 && S == 3 && stride == 1 && pad == 1 && g_conv_tile[0] == 0 && g_conv_stages[0] <= 0 &&
       conv3x3_halo_bn_ok(C, K, H, W) && conv3x3_halo_bn_fwd(x, w, y, N, H, W, bn.part, st))
     return;
+  // 1x1 / s2 projection from 256 channels with the BN statistics (ResNet-50 stage 2): the streaming expand kernel
+  // with a stride-2 row gather (gemm_expand.hip)
+  if (bn.mode == 1 && R == 1 && S == 1 && stride == 2 && pad == 0 && g_conv_tile[0] == 0 && g_conv_stages[0] <= 0 &&
+      conv1x1_s2_expand_bn(x, N, H, W, C, w, y, K, bn.part, st))
+    return;
   ConvGeom G = make_geom(N, H, W, C, K, R, S, stride, pad);
   const int M = N * G.P * G.Q;
   Epi e{y, K, 1, 1.f, 0.f, nullptr, 0};

@@ -34,12 +34,20 @@ using namespace gemm;
 constexpr int kXR = 64;  // rows per block
 constexpr int kXS = 3;   // A ring depth
 
+// Row gather of a 1x1 / stride-2 conv (S2): output row m = (n, p, q) of the P x Q grid reads input pixel (n, 2p, 2q)
+// of the H x W NHWC input (lda = channels)
+struct ExpandGather {
+  int H, W;
+  FastDiv fPQ, fQ;
+};
+
 // NT: non-temporal output stores; MINB: workgroups per CU the register allocation must allow (0: free)
-template <int K, bool NT, int MINB>
+template <int K, bool NT, int MINB, bool S2 = false>
 __global__ void __launch_bounds__(256, MINB > 0 ? MINB : 1) gemm_expand_bn_kernel(const bf16_t* __restrict__ A, long long lda,
                                                              const bf16_t* __restrict__ W, long long ldw,
                                                              bf16_t* __restrict__ C, long long ldc,
-                                                             float* __restrict__ part, int N, int nslice, int tiles) {
+                                                             float* __restrict__ part, int N, int nslice, int tiles,
+                                                             ExpandGather gth) {
   constexpr int KS = K / 32;                // MFMA k-steps
   constexpr int KH = K / 64;                // 64-deep halves of an A block (each a [64][64] KC image)
   constexpr int BLK = kXR * K * 2;          // bytes of one A block
@@ -74,17 +82,24 @@ __global__ void __launch_bounds__(256, MINB > 0 ? MINB : 1) gemm_expand_bn_kerne
   const int rb0 = base / nslice, gs = G / nslice;
   auto stage = [&](int it) {
     const int rb = rb0 + (it < my ? it : my - 1) * gs;
-    const char* src = (const char*)(A + (long long)rb * kXR * lda);
     lds_char* dst = smem + (it % kXS) * BLK;
 #pragma unroll
-    for (int h = 0; h < KH; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r0 = (wave * 2 + i) * 8, r = r0 + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
-        __builtin_amdgcn_global_load_lds((const void*)(src + ((long long)r * lda + h * 64 + c * 8) * 2),
-                                         (lds_void*)(dst + h * kXR * 128 + r0 * 128), 16, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const int r0 = (wave * 2 + i) * 8, r = r0 + (lane >> 3);
+      const int c = (lane & 7) ^ (r & 7);
+      long long arow = (long long)rb * kXR + r;  // the A row this lane's chunks come from
+      if constexpr (S2) {
+        uint32_t n, pq, pp, qq;
+        gth.fPQ.divmod((uint32_t)arow, n, pq);
+        gth.fQ.divmod(pq, pp, qq);
+        arow = ((long long)n * gth.H + 2 * (int)pp) * gth.W + 2 * (int)qq;
       }
+      const char* src = (const char*)(A + arow * lda + c * 8);
+#pragma unroll
+      for (int h = 0; h < KH; ++h)
+        __builtin_amdgcn_global_load_lds((const void*)(src + h * 128), (lds_void*)(dst + h * kXR * 128 + r0 * 128), 16,
+                                         0, 0);
+    }
   };
 
   float s[16], sq[16];
@@ -169,14 +184,14 @@ __global__ void __launch_bounds__(256, MINB > 0 ? MINB : 1) gemm_expand_bn_kerne
   }
 }
 
-template <int K, bool NT, int MINB>
+template <int K, bool NT, int MINB, bool S2 = false>
 int expand_grid(int nslice) {
   static int per_cu = -1, cus = 0;
   if (per_cu < 0) {
     int dev = 0;
     DTG_HIP_CHECK(hipGetDevice(&dev));
     DTG_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    DTG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_expand_bn_kernel<K, NT, MINB>, 256, 0));
+    DTG_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_expand_bn_kernel<K, NT, MINB, S2>, 256, 0));
     if (per_cu < 1) per_cu = 1;
   }
   int G = cus * per_cu;
@@ -336,7 +351,7 @@ bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long l
   if (nslice & (nslice - 1)) return false;  // 1, 2, 4, ... (grid divisibility)
   const int tiles = (M / kXR) * nslice;
   auto launch = [&](auto kern, int G) {
-    hipLaunchKernelGGL(kern, dim3(G), dim3(256), 0, st, A, lda, W, ldw, C, ldc, part, N, nslice, tiles);
+    hipLaunchKernelGGL(kern, dim3(G), dim3(256), 0, st, A, lda, W, ldw, C, ldc, part, N, nslice, tiles, ExpandGather());
   };
   // variant (A/B tool only): 0 default, 1 non-temporal stores, 2 registers for 3 workgroups per CU
   if (K == 64) {
@@ -350,6 +365,34 @@ bool gemm_expand_bn(const bf16_t* A, long long lda, const bf16_t* W, long long l
     else if (variant == 2) launch(gemm_expand_bn_kernel<128, false, 2>, expand_grid<128, false, 2>(nslice));
     else launch(gemm_expand_bn_kernel<128, false, 0>, expand_grid<128, false, 0>(nslice));
   }
+  DTG_LAUNCH_CHECK();
+  return true;
+}
+
+// 1x1 / stride-2 conv + BN statistics with 256 input channels (ResNet-50's stage-2 projection, 56x56x256 -> 28x28x512
+// at batch 1024: 414 us on the implicit-GEMM conv, 508 TF/s): the K = 256 expand kernel with the stride-2 row
+// gather.  x [Nb, H, W, 256] NHWC, w [Kout][256], y [Nb * H/2 * W/2][Kout].  Switch for the A/B tools.
+static int g_expand_s2 = 1;
+void gemm_expand_s2_set(int on) { g_expand_s2 = on; }
+
+bool conv1x1_s2_expand_bn(const bf16_t* x, int Nb, int H, int W, int Cin, const bf16_t* w, bf16_t* y, int Kout,
+                          float* part, hipStream_t st) {
+  if (!g_expand_s2 || Cin != 256 || Kout % 256 || (H & 1) || (W & 1)) return false;
+  const int P = H / 2, Q = W / 2;
+  const long long M = (long long)Nb * P * Q;
+  if (M % kXR || M >= (1LL << 31) || (long long)Nb * H * W * Cin >= (1LL << 40)) return false;
+  if (M * Kout < (1LL << 24)) return false;
+  const int nslice = Kout / 256;
+  if (nslice & (nslice - 1)) return false;
+  ExpandGather gth;
+  gth.H = H;
+  gth.W = W;
+  gth.fPQ = FastDiv((uint32_t)(P * Q));
+  gth.fQ = FastDiv((uint32_t)Q);
+  const int tiles = (int)(M / kXR) * nslice;
+  hipLaunchKernelGGL((gemm_expand_bn_kernel<256, false, 0, true>), dim3(expand_grid<256, false, 0, true>(nslice)),
+                     dim3(256), 0, st, x, (long long)Cin, w, (long long)Cin, y, (long long)Kout, part, Kout, nslice, tiles,
+                     gth);
   DTG_LAUNCH_CHECK();
   return true;
 }

@@ -111,6 +111,32 @@ def _pack_mask(x, mean, inv, gamma, beta):
     return (m << torch.arange(8, device=x.device, dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
 
 
+# the 1x1 / stride-2 projection from 256 channels on the streaming expand kernel with a row gather
+# (gemm_expand.hip conv1x1_s2_expand_bn; M * K >= 2^24 and M % 64 == 0): against fp32 and the implicit-GEMM conv
+@pytest.mark.parametrize("N,H,K", [(48, 56, 512), (96, 28, 1024), (2048, 8, 512)])
+def test_conv1x1_s2_expand_bn(N, H, K):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    C = 256
+    x = torch.randn(N, H, H, C, generator=g).to(dev, torch.bfloat16)
+    w = torch.randn(K, 1, 1, C, generator=g).mul_(C ** -0.5).to(dev, torch.bfloat16)
+    L = lib()
+    y, part = L.conv_fwd_bn(x, w, 2, 0)
+    yr = F.conv2d(x.permute(0, 3, 1, 2).float(), w.permute(0, 3, 1, 2).float(), stride=2).permute(0, 2, 3, 1)
+    assert _rel(y, yr) < 1e-2
+    yf = y.float().reshape(-1, K)
+    s, q = _bn_stats(part, K)
+    assert _rel(s, yf.sum(0)) < 1e-4 and _rel(q, (yf * yf).sum(0)) < 1e-4
+    L.gemm_expand_s2_set(0)
+    try:
+        y0, part0 = L.conv_fwd_bn(x, w, 2, 0)
+    finally:
+        L.gemm_expand_s2_set(1)
+    assert _rel(y, y0) < 2e-3
+    s0, q0 = _bn_stats(part0, K)
+    assert _rel(s, s0) < 1e-3 and _rel(q, q0) < 1e-4
+
+
 @pytest.mark.parametrize("C,K,H,R,st,pad", [(64, 64, 14, 3, 1, 1), (64, 64, 16, 3, 1, 1), (128, 128, 14, 3, 2, 1),
                                             (64, 256, 8, 1, 1, 0),
                                             (256, 512, 7, 3, 1, 1)])
