@@ -945,6 +945,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("bucket") = pybind11::none(), pybind11::arg("factor") = 1.0);
   m.def("stem_stream_set", [](int64_t on) { dtg::stem_stream_set((int)on); });
   m.def("gemm_expand_k256_set", [](int64_t on) { dtg::gemm_expand_k256_set((int)on); });
+  m.def("stem_pool_rows_set", [](int64_t on) { dtg::stem_pool_rows_set((int)on); });
   m.def("gemm_expand_s2_set", [](int64_t on) { dtg::gemm_expand_s2_set((int)on); });
   m.def("conv_halo_fwd_set", [](int64_t on) { dtg::conv3x3_halo_fwd_set((int)on); });
   m.def("conv_halo_dgrad_set", [](int64_t on) { dtg::conv3x3_halo_dgrad_set((int)on); });

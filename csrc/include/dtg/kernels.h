@@ -280,6 +280,7 @@ int conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int N, int H, int 
                int stride, int pad, float beta, hipStream_t st, const BnEpi& bn = BnEpi(),
                const bf16_t* wT = nullptr, int zero_rest = 1);
 void stem_stream_set(int on);  // the streaming stem conv (gemm_expand.hip) on / off (A/B tools)
+void stem_pool_rows_set(int on);  // stem max-pool forward: the row-walking kernel (1, default) or row-parallel (0)
 void gemm_expand_k256_set(int on);  // the streaming expand GEMM for K = 256 (gemm_expand.hip) on / off (A/B tools)
 void gemm_expand_s2_set(int on);    // the stride-2 1x1 projection on the expand kernel (gemm_expand.hip) on / off
 bool conv1x1_s2_expand_bn(const bf16_t* x, int Nb, int H, int W, int Cin, const bf16_t* w, bf16_t* y, int Kout,

@@ -114,6 +114,88 @@ __global__ void __launch_bounds__(256) stem_pool_fwd_kernel(const bf16_t* __rest
   }
 }
 
+// The same pass for ResNet's geometry (3x3 / stride 2 / pad 1, H = 2P, W = 2Q) walking down a segment of pooled rows:
+// a thread owns (n, q, 8 channels, kPoolSeg rows) and keeps the window's bottom input row (2p + 1) in registers as
+// the next window's top row (2(p + 1) - 1), so every input row is loaded once per segment instead of by the two
+// windows that share it (the row-parallel form above re-reads part of y through HBM): 611 -> 553 us at batch 1024
+// (profiles/r06_pool_rows; prefetching the next window's rows as well measured 590 us -- fewer waves resident).
+// Window order, tie rule and outputs are those of stem_pool_fwd_kernel.
+constexpr int kPoolSeg = 14;
+__global__ void __launch_bounds__(256) stem_pool_fwd_rows_kernel(const bf16_t* __restrict__ y,
+                                                                 const float* __restrict__ coef,
+                                                                 bf16_t* __restrict__ out, uint8_t* __restrict__ idx,
+                                                                 bf16_t* __restrict__ yam, StemGeom g, int nseg) {
+  const unsigned c8n = g.C >> 3;
+  const unsigned total = (unsigned)g.N * nseg * g.Q * c8n;  // < 2^31 (host check)
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % c8n);
+    unsigned t = i / c8n;
+    const int q = (int)(t % (unsigned)g.Q);
+    t /= (unsigned)g.Q;
+    const int seg = (int)(t % (unsigned)nseg);
+    const int n = (int)(t / (unsigned)nseg);
+    const int p0 = seg * kPoolSeg, p1 = min(g.P, p0 + kPoolSeg);
+    float sc[8], sf[8];
+    load8_f32(coef + c8 * 8, sc);
+    load8_f32(coef + g.C + c8 * 8, sf);
+    const int w0 = 2 * q - 1;
+    const bool okc[3] = {w0 >= 0, true, true};  // w0 + 1, w0 + 2 <= 2Q - 1 < W
+    const bf16_t* yn = y + (long long)n * g.H * g.W * g.C + c8 * 8;
+    auto ld = [&](int h, int cc) -> uint4 {
+      return *reinterpret_cast<const uint4*>(yn + ((long long)h * g.W + (okc[cc] ? w0 + cc : 0)) * g.C);
+    };
+    uint4 top[3];
+    const bool top_ok0 = p0 > 0;
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) top[cc] = ld(top_ok0 ? 2 * p0 - 1 : 0, cc);
+    bool top_ok = top_ok0;
+    for (int p = p0; p < p1; ++p) {
+      uint4 mid[3], bot[3];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        mid[cc] = ld(2 * p, cc);
+        bot[cc] = ld(2 * p + 1, cc);
+      }
+      float m[8];
+      uint32_t ym[4] = {0u, 0u, 0u, 0u};
+      uint32_t am[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m[k] = -INFINITY;
+      auto take = [&](const uint4& raw, bool ok, uint8_t wi) {
+        float v[8];
+        gemm::unpack8_bf16(raw, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = ok ? bn_relu_bf(v[k], sc[k], sf[k]) : -INFINITY;
+          if (a > m[k]) {  // strict: the first maximum in window order wins ties
+            m[k] = a;
+            am[k >> 2] = (am[k >> 2] & ~(0xffu << (8 * (k & 3)))) | ((uint32_t)wi << (8 * (k & 3)));
+            const uint32_t word = (k >> 1) == 0 ? raw.x : (k >> 1) == 1 ? raw.y : (k >> 1) == 2 ? raw.z : raw.w;
+            ym[k >> 1] = (k & 1) ? ((ym[k >> 1] & 0xffffu) | (word & 0xffff0000u))
+                                 : ((ym[k >> 1] & 0xffff0000u) | (word & 0xffffu));
+          }
+        }
+      };
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) take(top[cc], top_ok && okc[cc], (uint8_t)cc);
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) take(mid[cc], okc[cc], (uint8_t)(3 + cc));
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) take(bot[cc], okc[cc], (uint8_t)(6 + cc));
+      const long long o = (((long long)n * g.P + p) * g.Q + q) * g.C + c8 * 8;
+      store8_bf16(out + o, m);
+      *reinterpret_cast<uint2*>(idx + o) = make_uint2(am[0], am[1]);
+      if (yam) *reinterpret_cast<uint4*>(yam + o) = make_uint4(ym[0], ym[1], ym[2], ym[3]);
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) top[cc] = bot[cc];
+      top_ok = true;
+    }
+  }
+}
+
+static int g_pool_rows = 1;
+void stem_pool_rows_set(int on) { g_pool_rows = on; }
+
 // dp at input pixel m = (n, h, w), channels c0..c0+7: sum of the pooled gradients routed to it,
 // masked by relu'(bn(y)) (yv = y at the pixel, sc/sf = the forward scale/shift).  With k <= 2s (the
 // host checks it) a pixel lies in at most 2 x 2 windows: the pooled rows p_hi - 1, p_hi and columns
@@ -578,8 +660,14 @@ void stem_bn_pool_fwd(const bf16_t* y, const float* part, const float* gamma, co
                                                          sinv, momentum, eps, coef, nullptr, nullptr, 0); DTG_LAUNCH_CHECK();
   const StemGeom g = stem_geom(N, H, W, C, k, s, pad, P, Q);
   const long long total = (long long)N * P * Q * (C / 8);
-  // 3x3 windows (ResNet): the unrolled form with raw-vector loads; other windows: the runtime loop
-  if (k == 3)
+  // 3x3 / 2 / 1 windows over an even-sized input (ResNet): the row-walking form; other 3x3 windows: the unrolled
+  // form with raw-vector loads; other windows: the runtime loop
+  if (g_pool_rows && k == 3 && s == 2 && pad == 1 && H == 2 * P && W == 2 * Q) {
+    const int nseg = (P + kPoolSeg - 1) / kPoolSeg;
+    const long long tr = (long long)N * nseg * Q * (C / 8);
+    hipLaunchKernelGGL(stem_pool_fwd_rows_kernel, dim3(grid_for(tr, 256, 8192)), dim3(256), 0, st, y, coef, out, idx,
+                       yam, g, nseg);
+  } else if (k == 3)
     hipLaunchKernelGGL(stem_pool_fwd_kernel<3>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, yam, g);
   else
     hipLaunchKernelGGL(stem_pool_fwd_kernel<0>, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, y, coef, out, idx, yam, g);

@@ -475,3 +475,39 @@ def test_wgrad_side_stream_accumulates_into_existing_grad(monkeypatch):
     rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
     errs = [rel(a, b) for a, b in zip(res[1], res[0])]
     assert max(errs) < 1e-2, errs
+
+
+@pytest.mark.parametrize("N,H", [(4, 112), (3, 30), (2, 58)])
+def test_stem_pool_rows_kernel_matches_row_parallel(N, H):
+    """The row-walking stem BN + ReLU + 3x3/2 max-pool forward (stem.hip stem_pool_fwd_rows_kernel: a thread walks a
+    segment of pooled rows and carries the shared input row in registers) equals the row-parallel kernel bit for
+    bit -- outputs, argmax indices (ties: many ReLU zeros and repeated values, first maximum in window order) and
+    the saved y at the argmax -- including a segment shorter than the 14-row default (H = 30 -> 15 pooled rows)."""
+    import torch.nn.functional as F
+    from dtg.ops._native import lib
+    dev = torch.device("cuda")
+    L = lib()
+    C = 64
+    g = torch.Generator(device="cpu").manual_seed(H)
+    y = (torch.randint(-4, 5, (N, H, H, C), generator=g).float() * 0.5).to(dev, torch.bfloat16)
+    yf = y.float().view(-1, C)
+    part = torch.zeros(32, 2, C, device=dev)
+    part[0, 0] = yf.sum(0)
+    part[0, 1] = (yf * yf).sum(0)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(dev)
+    beta = (torch.rand(C, generator=g) - 0.5).to(dev)
+    res = {}
+    for on in (0, 1):
+        L.stem_pool_rows_set(on)
+        try:
+            rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+            res[on] = L.stem_bn_pool_fwd(y, part, gamma, beta, rm, rv, 0.1, 1e-5, 3, 2, 1, save_yam=True)
+        finally:
+            L.stem_pool_rows_set(1)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    # and against torch: max_pool2d(relu(bn(y)))
+    mean, var = yf.mean(0), yf.var(0, unbiased=False)
+    a = torch.relu((y.float() - mean) / torch.sqrt(var + 1e-5) * gamma + beta).bfloat16().float()
+    ref = F.max_pool2d(a.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.allclose(res[1][0].float(), ref, atol=2e-2, rtol=1e-2)

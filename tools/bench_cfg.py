@@ -37,6 +37,8 @@ if os.environ.get("DTG_AB_EXPAND256"):  # 0: the tiled BN-statistics GEMM for K 
     lib().gemm_expand_k256_set(int(os.environ["DTG_AB_EXPAND256"]))
 if os.environ.get("DTG_AB_EXPAND_S2"):  # 0: the implicit-GEMM conv for the stage-2 1x1 / s2 projection forward
     lib().gemm_expand_s2_set(int(os.environ["DTG_AB_EXPAND_S2"]))
+if os.environ.get("DTG_AB_POOL_ROWS"):  # 0: the row-parallel stem max-pool forward instead of the row-walking one
+    lib().stem_pool_rows_set(int(os.environ["DTG_AB_POOL_ROWS"]))
 if os.environ.get("DTG_AB_BN_CFG"):
     lib().gemm_bn_force_cfg(int(os.environ["DTG_AB_BN_CFG"]))
 for item in filter(None, os.environ.get("DTG_AB_STAGES", "").split(",")):  # "<pass>:<schedule>", conv_set_stages
