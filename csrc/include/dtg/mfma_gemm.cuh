@@ -76,10 +76,17 @@ __device__ __forceinline__ const void* sel(bool ok, const void* p) {
   return (const void*)(ok ? a : z);
 }
 
-// swizzle of the 16-B chunk index of an MC row (CH chunks): keeps 32-B pairs together and makes
-// the 8 rows read by one ds_read_b64_tr_b16 half-wave distinct where the row is wide enough
+// swizzle of the 16-B chunk index of an MC row (CH chunks): makes the 8 rows read by one ds_read_b64_tr_b16
+// half-wave (rows 8g + q, g in {0, 1}, q in 0..3) hit distinct banks.  A half-wave reads, per row, one aligned
+// pair of chunks (c, c + 1) and rows of equal parity share the same 32 banks, so the swizzle's bits [2:1] must
+// differ over rows {0, 2, 8, 10} (and {1, 3, 9, 11}).  For 64-row tiles (CH = 8) that takes row bits 1 and 3
+// (plus row bit 0 as chunk bit 0, which also spreads the 16-B row reads of a 16-row block over all 8 chunks);
+// the wider rows keep the pair-preserving form.  (The earlier CH = 8 form folded row bit 3 away: rows 0 and 8
+// read the same banks, a 2-way conflict on every 64-row MC fragment read -- 57 % / 46 % of the attention forward /
+// backward's LDS cycles were bank conflicts, profiles/r06_lds_swz.)
 template <int CH>
 __device__ __forceinline__ int mc_swz(int k) {
+  if constexpr (CH == 8) return (((k >> 3) & 1) << 2) | (((k >> 1) & 1) << 1) | (k & 1);
   return ((((k & 3) | (((k >> 3) & 1) << 2)) << 1) & (CH - 1));
 }
 

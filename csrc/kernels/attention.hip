@@ -208,14 +208,15 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
     }
     lds_fence();  // the scratch is rewritten by the next chunk
   }
-  // finalize: O^T / l -> scratch (row-major [16 q][64 d], 4 consecutive d per lane and block) -> 16-B global stores
+  // finalize: O^T / l -> scratch ([16 q][64 d], 4 consecutive d per lane and block; 16-B chunks XOR-swizzled by the
+  // row, so the 16 rows of a store do not all hit the same banks) -> 16-B global stores
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float il = 1.f / l;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float v[4] = {o[j][0] * il, o[j][1] * il, o[j][2] * il, o[j][3] * il};
-    st4_bf16(scr + qi * 128 + (j * 16 + 4 * g) * 2, v);
+    st4_bf16(scr + qi * 128 + (((2 * j + (g >> 1)) ^ (qi & 7)) << 4) + (g & 1) * 8, v);
   }
   if (g == 0) lse[(long long)bh * S + q0 + qi] = m + __logf(l);
   lds_fence();
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(64 * kFwdWaves) attn_fwd_kernel(const bf16_t* 
   for (int i = 0; i < 2; ++i) {
     const int c = lane + 64 * i;  // 128 chunks of 16 B: row c/8, chunk c%8
     const int row = c >> 3, ch = c & 7;
-    const v8bf v = *reinterpret_cast<const lds_v8bf*>(scr + row * 128 + ch * 16);
+    const v8bf v = *reinterpret_cast<const lds_v8bf*>(scr + row * 128 + ((ch ^ (row & 7)) << 4));
     *reinterpret_cast<v8bf*>(out + ((long long)b * S + q0 + row) * H + h * 64 + ch * 8) = v;
   }
 }
